@@ -1,0 +1,221 @@
+"""Benchmark: SIR PMCMC particle-steps/s on MI355X (BASELINE.json metric, config 2).
+
+A "step" is one Metropolis-Hastings iteration of every chain on this rank: host proposals, one batched
+GPU particle filter (N=10,000 particles x T=200 observations per chain, SIR, binomial observations,
+population 10,000), on-device path sampling, host accept/reject.  value = N x T x (chains that ran a
+filter) over all ranks / max-over-ranks wall time of the K timed steps (inputs resident in HBM).
+
+Multi-GPU: one process per GPU (torch.distributed.run); chains are independent, so each rank runs its
+own `--chains` chains with no collective on the data path; the posterior draws of the timed steps are
+all-gathered over RCCL at the end of the timed region (pmcmc chain gather).
+
+Also reported: roofline of the dominant kernel (pf_step_kernel, HIP-event timed on the engine's stream),
+and a CPU baseline (the oracle C restatement, OpenMP, on a bounded sample) on rank 0 at N=1.
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "stochastic-epidemic-modelling_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--chains", type=int, default=int(os.environ.get("EPIPF_BENCH_CHAINS", 16)),
+                    help="independent MH chains per GPU (batched in one launch per filter step)")
+    ap.add_argument("--particles", type=int, default=10000)
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--single-chain", action="store_true", help="also time 1 chain/GPU (extra field)")
+    return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def cpu_baseline(Y, meta, N, seconds):
+    """Oracle (C restatement of the reference filter, OpenMP over particles) on the GPU box's host.
+    Sample: whole cfg filters (N particles x T steps) repeated until `seconds` elapse (at least one)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    threads = min(16, os.cpu_count() or 1)
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    oracle.build()
+    th = np.array(meta["theta"])
+    t0 = time.perf_counter()
+    n = 0
+    ev = 0
+    while True:
+        o = oracle.particle_filter(Y, meta["model"], th, meta.get("observations", False), meta["probs"], N,
+                                   meta["n_population"], meta["mu"], key=7, filter_index=n)
+        n += 1
+        ev += o["events"]
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=n * N * Y.shape[0] / dt, unit="particle-steps/s", cores=oracle.num_threads(), kind="port",
+                sample=f"{n} full filter(s) of config 2 (N={N}, T={Y.shape[0]}), {dt:.1f}s, {ev / dt:.3g} events/s, "
+                       f"host CPU: {cpu_model()}")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    import torch
+
+    from epipf import datasets
+    from epipf.pmcmc import ChainSampler, chain_key
+
+    Y, meta = datasets.benchmark_dataset(args.config)
+    N, T = args.particles, Y.shape[0]
+    C = args.chains
+    gid = [rank * C + c for c in range(C)]
+    sampler = ChainSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=args.warmup + args.steps + 1,
+                           observations=meta.get("observations", False), probs=meta["probs"], n_particles=N,
+                           n_population=meta["n_population"], mu=meta["mu"],
+                           rngs=[np.random.RandomState(args.seed + g) for g in gid],
+                           keys=[chain_key(args.seed, g) for g in gid], device=local, mh_ratio="log")
+    eng = sampler.eng
+    sampler.initialise()
+    for _ in range(args.warmup):
+        sampler.step()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    eng.reset_stats()
+    eng.set_profiling(True)
+    barrier()
+    t0 = time.perf_counter()
+    filters = 0
+    for _ in range(args.steps):
+        filters += sampler.step()
+    # end of run: gather the posterior draws of every rank's chains over RCCL (xGMI)
+    draws = np.concatenate([sampler.thetas[:, :sampler.i].reshape(C, -1),
+                            sampler.loglik[:, :sampler.i]], axis=1)
+    if dist is not None:
+        local_t = torch.from_numpy(draws).to(f"cuda:{local}")
+        out = [torch.empty_like(local_t) for _ in range(world)]
+        dist.all_gather(out, local_t)
+        gathered = torch.cat(out).cpu().numpy()
+    else:
+        gathered = draws
+    barrier()
+    dt = time.perf_counter() - t0
+    eng.set_profiling(False)
+    st = eng.stats()
+
+    # max over ranks of the wall time; sum of filters
+    if dist is not None:
+        tt = torch.tensor([dt, float(filters)], dtype=torch.float64, device=f"cuda:{local}")
+        mx = tt.clone()
+        dist.all_reduce(mx[0:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(mx[1:2], op=dist.ReduceOp.SUM)
+        dt, filters_all = float(mx[0]), int(mx[1])
+    else:
+        filters_all = filters
+    value = filters_all * N * T / dt
+
+    # roofline of the dominant kernel: pf_step_kernel (resample + gather + SSA + weight + in-block scan)
+    launches = max(1, st["step_launches"])
+    avg_launch_s = st["step_ms"] / 1e3 / launches
+    units_per_launch = filters * N / args.steps                      # particle-steps per launch (all chains)
+    bytes_per_unit = 8 * 3 + 40                                       # 8C+40 with C=3
+    achieved = units_per_launch * bytes_per_unit / avg_launch_s / 1e9
+    traffic = None
+    pmc_path = os.path.join(REPO, "profiles", "pmc_step_kernel.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    events_per_s = st["events"] / (st["step_ms"] / 1e3) if st["step_ms"] > 0 else None
+
+    single = None
+    if args.single_chain and rank == 0 and world == 1:
+        s1 = ChainSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=args.steps + 2, probs=meta["probs"],
+                          n_particles=N, n_population=meta["n_population"], mu=meta["mu"],
+                          rngs=[np.random.RandomState(args.seed)], keys=[chain_key(args.seed, 0)], device=local,
+                          mh_ratio="log")
+        s1.initialise()
+        s1.step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        f1 = sum(s1.step() for _ in range(args.steps))
+        torch.cuda.synchronize()
+        single = f1 * N * T / (time.perf_counter() - t1)
+
+    base = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        base = cpu_baseline(Y, meta, N, args.cpu_baseline_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "particle-steps/sec (N_particles x T_obs x MH-iters) on SIR PMCMC",
+            "value": value,
+            "unit": "particle-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (config-2 ODE SIR y0=(9980,20,0), beta=.25, gamma=.1, 200 daily rows, "
+                    "binomial thinning p=.1, RandomState(1)); Philox-keyed filter draws",
+            "config": {"workload": f"BASELINE config {args.config}: SIR PMCMC, N={N} particles, pop=1e4, "
+                                   f"{T} obs, {C} independent chains per GPU",
+                       "particles": N, "T_obs": T, "chains_per_gpu": C, "population": meta["n_population"],
+                       "parallelism": f"chains sharded over {world} GPU(s), RCCL all-gather of draws at end"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "pf_step_kernel", "avg_launch_us": avg_launch_s * 1e6,
+                         "bytes_per_particle_step": bytes_per_unit, "particle_steps_per_launch": units_per_launch},
+            "events_per_s": events_per_s,
+            "resample_fallbacks": st["resample_fallbacks"],
+            "gathered_draws_shape": list(gathered.shape),
+            "cpu_baseline": base,
+        }
+        if single is not None:
+            line["single_chain_value"] = single
+        if base is not None:
+            line["speedup_vs_cpu_baseline"] = value / base["value"]
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

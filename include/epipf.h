@@ -1,0 +1,132 @@
+/*
+ * epipf.h -- C ABI of the MI355X particle-filter engine (libepipf.so).
+ *
+ * The reference (GeorgeEfstathiadis/Stochastic-Epidemic-Modelling) is pure Python and has no FFI;
+ * its seams are plain Python calls.  These entry points replace, one for one:
+ *
+ *   epipf_run            pmcmc.py:123-233  particle_filter(Y, type_model, theta_proposal, observations,
+ *                                          probs, n_particles, n_population, mu, jobs)
+ *                        -- batched over independent chains; the per-particle joblib dispatch of
+ *                           pmcmc.py:200-220 becomes one GPU lane per particle.
+ *   epipf_copy_history   pmcmc.py:151-152,233  the hidden_process [T,N,C] / ancestry_matrix [T,N] outputs
+ *   epipf_path_sample    pmcmc.py:236-248  particle_path_sampler(hidden_process, ancestry_matrix)
+ *                        (the uniform pick np.random.randint(0, N) stays on the host RNG: `chosen`)
+ *   epipf_simulate       gillespie_algo.py:10-75 / 78-146 / 148-233  sir_simulate / seir_simulate /
+ *                        sir_subgroups_simulate(..., last_values_only=True), batched over states
+ *   epipf_resample       pmcmc.py:185-190  normalise + np.random.choice(range(N), N, p=w/sum(w)) with
+ *                        caller-supplied uniforms (bit-exact to numpy's legacy choice)
+ *
+ * The host wrapper (stochastic-epidemic-modelling_amd/epipf/) binds these with ctypes and keeps
+ * the reference's Python signatures.  Conventions:
+ *   - all pointers are HOST pointers to C-contiguous arrays owned by the caller; the context owns and
+ *     reuses every device buffer (observations and history stay resident in HBM across calls);
+ *   - return value 0 = EPIPF_OK, negative = error (message via epipf_last_error()); nothing throws;
+ *   - one context per device; calls on one context must be serialised by the caller;
+ *   - random numbers come from the keyed Philox4x32-10 stream documented in DESIGN.md §3
+ *     (key = 64-bit seed per chain, filter_index = one per particle-filter call).
+ */
+#ifndef EPIPF_H
+#define EPIPF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EPIPF_ABI_VERSION 1
+
+/* return codes */
+#define EPIPF_OK 0
+#define EPIPF_EINVAL (-1)   /* bad argument / shape */
+#define EPIPF_EHIP (-2)     /* HIP runtime error */
+#define EPIPF_ENOMEM (-3)   /* device allocation failed */
+#define EPIPF_ESTATE (-4)   /* call order (e.g. path sample before any run) */
+
+/* per-chain status written by epipf_run */
+#define EPIPF_STATUS_OK 0
+#define EPIPF_STATUS_DEGENERATE 1 /* all weights 0 or NaN at some step: reference returns (None, None, None) */
+#define EPIPF_STATUS_SKIPPED 2    /* chain was inactive in this call (active[c] == 0) */
+
+/* models: pmcmc.py:116-120 ModelType */
+#define EPIPF_SIR 0
+#define EPIPF_SEIR 1
+#define EPIPF_SIR_SUBGROUPS 2
+#define EPIPF_SIR_SUBGROUPS2 3
+
+/* observation models: pmcmc.py:178-181 (observations=False / True) */
+#define EPIPF_OBS_BINOMIAL 0
+#define EPIPF_OBS_NORMAL 1
+
+/* resampling: multinomial is the reference's (pmcmc.py:188); systematic is opt-in and changes results */
+#define EPIPF_RESAMPLE_MULTINOMIAL 0
+#define EPIPF_RESAMPLE_SYSTEMATIC 1
+
+typedef struct epipf_ctx epipf_ctx;
+
+typedef struct {
+    double step_ms;              /* HIP-event time of the fused resample+propagate+weight kernels (profiling on) */
+    int64_t step_launches;       /* number of such launches timed */
+    double init_ms;              /* HIP-event time of the init kernels (profiling on) */
+    int64_t init_launches;
+    int64_t events;              /* accepted Gillespie events (profiling on) */
+    int64_t particle_steps;      /* N x T_obs x chains that ran a filter */
+    int64_t filters;             /* chain-filters run */
+    int64_t resample_fallbacks;  /* draws resolved by the sequential bit-exact path */
+} epipf_stats;
+
+/* groups: G for the subgroup models (1 <= G <= 4), ignored (1) for SIR/SEIR.
+ * t_max: largest T (observation rows) a run may use; max_chains: largest batch of independent filters. */
+int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_particles, int t_max,
+                 int max_chains);
+void epipf_destroy(epipf_ctx* ctx);
+
+/* Y: [T*K] row-major observed counts (K = C, or 3 for SIR_SUBGROUPS2).  Uploaded once, kept in HBM. */
+int epipf_set_observations(epipf_ctx* ctx, const double* Y, int T, int K);
+
+/* n_population, mu: [G] (pmcmc.py:129-131; G = 1 for SIR/SEIR).  n_population must be integral. */
+int epipf_set_population(epipf_ctx* ctx, const double* n_population, const double* mu);
+
+/* Run n_chains independent particle filters (one per chain) over the resident observations.
+ *   theta  [n_chains*d]: SIR (beta, gamma); SEIR (beta, alpha, gamma); subgroups beta[G][G] row-major + gamma
+ *   probs  [n_chains]   : binomial detection probability, or the normal-noise ratio (observations=True)
+ *   keys   [n_chains]   : Philox key per chain;  filter_index [n_chains]: stream index of this call
+ *   active [n_chains] or NULL: 0 marks a chain that runs nothing this call (status SKIPPED)
+ *   log_zetas_out [n_chains*T] or NULL: log of the reference's zetas (zetas = exp(log_zetas))
+ *   status_out [n_chains]: EPIPF_STATUS_*                                                               */
+int epipf_run(epipf_ctx* ctx, int n_chains, const double* theta, int d, int obs_model, const double* probs,
+              const uint64_t* keys, const uint32_t* filter_index, const int32_t* active, int resample_mode,
+              double* log_zetas_out, int32_t* status_out);
+
+/* Copy the last run's history: hidden [n_chains*T*N*C] int32 (compartment counts), ancestry [n_chains*T*N]
+ * int32 (row 0 zeros, as pmcmc.py:152).  Either pointer may be NULL. */
+int epipf_copy_history(epipf_ctx* ctx, int n_chains, int32_t* hidden_out, int32_t* ancestry_out);
+
+/* On-device particle_path_sampler (pmcmc.py:236-248, including its ancestry[p] indexing) for each chain of
+ * the last run; chosen [n_chains] is the host's np.random.randint(0, N) draw.  traj_out [n_chains*T*C]. */
+int epipf_path_sample(epipf_ctx* ctx, int n_chains, const int32_t* chosen, int32_t* traj_out);
+
+/* Batched last-value SSA from n states [n*C] over [0, max_time] (gillespie_algo.py *_simulate with
+ * last_values_only=True).  State j draws SSA event k from counter (k, j, step, filter_index). */
+int epipf_simulate(epipf_ctx* ctx, int n, const int32_t* states_in, const double* theta, int d,
+                   double max_time, uint64_t key, uint32_t filter_index, uint32_t step, int32_t* states_out,
+                   int64_t* events_out);
+
+/* Standalone resampler: out[j] = numpy legacy choice(range(n), n, p=w/sum(w)) given uniforms u[j].
+ * Returns EPIPF_STATUS_DEGENERATE (as a positive value) where numpy raises ValueError. */
+int epipf_resample(epipf_ctx* ctx, int n, const double* w, const double* u, int32_t* out,
+                   int64_t* fallbacks_out);
+
+int epipf_set_profiling(epipf_ctx* ctx, int enable);
+int epipf_get_stats(epipf_ctx* ctx, epipf_stats* out);
+int epipf_reset_stats(epipf_ctx* ctx);
+
+const char* epipf_last_error(void);
+int epipf_abi_version(void);
+int epipf_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EPIPF_H */

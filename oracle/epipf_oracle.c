@@ -1,0 +1,336 @@
+/*
+ * epipf_oracle.c -- CPU restatement of the reference particle filter (TEST INFRASTRUCTURE).
+ *
+ * THIS IS THE ORACLE, NOT THE PRODUCT.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it, and only as the checker / the timed CPU baseline.  The product
+ * path (stochastic-epidemic-modelling_amd/csrc, libepipf.so) never links or calls this file.
+ *
+ * It restates, operation for operation, the arithmetic of
+ *   /root/reference/gillespie_algo.py:10-75   sir_simulate            (SSA, 2 channels)
+ *   /root/reference/gillespie_algo.py:78-146  seir_simulate           (SSA, 3 channels)
+ *   /root/reference/gillespie_algo.py:148-233 sir_subgroups_simulate  (SSA, G*G+G channels)
+ *   /root/reference/pmcmc.py:123-233          particle_filter         (init, weight, resample, propagate)
+ * with every random number taken from the keyed Philox4x32-10 stream defined in oracle/philox.py
+ * (the reference is pinned to the same stream by the RNG-injection shim in
+ * tests/golden/make_golden.py, which runs the unmodified reference functions).
+ *
+ * Third-party arithmetic restated here (absent as C in /root/reference):
+ *   numpy 2.2 legacy RandomState.exponential(scale) = scale * (-log(1.0 - U))   (glibc log)
+ *   numpy 2.2 legacy RandomState.choice(a, size, p)  = searchsorted(cumsum(p)/cumsum(p)[-1], U, 'right')
+ *   scipy 1.15 binom.pmf(k, n, p)  -> exp(lgamma(n+1) - lgamma(k+1) - lgamma(n-k+1) + k log p + (n-k) log1p(-p))
+ *                                     (Boost in scipy; agrees to ~1e-11 relative)
+ *   scipy 1.15 norm.pdf(y, loc, scale) = exp(-z*z/2) / 2.5066282746310002 / scale,  z = (y-loc)/scale
+ *
+ * Compile with -ffp-contract=off: every multiply/add/divide must round exactly like CPython/numpy.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+enum { M_SIR = 0, M_SEIR = 1, M_SUBGROUPS = 2, M_SUBGROUPS2 = 3 };
+enum { OBS_BINOMIAL = 0, OBS_NORMAL = 1 };
+enum { RS_MULTINOMIAL = 0, RS_SYSTEMATIC = 1 };
+enum { DOM_SSA = 0, DOM_RESAMPLE = 1, DOM_INIT = 2 };
+#define MAXG 8
+#define MAXC (3 * MAXG)
+#define MAXCH (MAXG * MAXG + MAXG)
+
+/* ------------------------------------------------------------------ Philox4x32-10 */
+static void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint64_t key, uint32_t out[4]) {
+    uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1, n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+static double u01(uint32_t lo, uint32_t hi) {
+    uint64_t x = ((uint64_t)hi << 32) | lo;
+    return (double)(x >> 11) * (1.0 / 9007199254740992.0);
+}
+void oracle_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint64_t key, uint32_t* out) {
+    philox(c0, c1, c2, c3, key, out);
+}
+
+/* ------------------------------------------------------------------ model description */
+typedef struct {
+    int model, G, C;          /* C = compartments per particle (3, 4, 3G) */
+    double theta[MAXCH + 1];  /* SIR: beta,gamma  SEIR: beta,alpha,gamma  groups: beta[G][G] row-major, gamma */
+} model_t;
+
+/* Gillespie direct method over [0, max_time], gillespie_algo.py.  State in x[] (ints held as doubles,
+ * exactly as the reference holds them in float64).  Returns the number of accepted events. */
+static long ssa(const model_t* m, double* x, double max_time, uint64_t key, uint32_t f, uint32_t ptag,
+                uint32_t j) {
+    uint32_t r[4];
+    double t = 0.0;
+    uint32_t k = 0;
+    long nev = 0;
+    if (m->model == M_SIR) {
+        const double beta = m->theta[0], gamma = m->theta[1];
+        double S = x[0], I = x[1], R = x[2];
+        const double N = (S + I) + R;                                   /* gillespie_algo.py:35 */
+        while (I > 0.0) {                                               /* :48 */
+            double a0 = ((beta * S) * I) / N;                           /* :38 */
+            double a1 = gamma * I;                                      /* :39 */
+            double as = a0 + a1;                                        /* builtin sum, :62 */
+            philox(k++, j, ptag, f, key, r);
+            double tau = (1.0 / as) * (-log(1.0 - u01(r[0], r[1])));    /* np.random.exponential, :62 */
+            double p0 = a0 / as, p1 = a1 / as;                          /* p=a/sum(a), :63 */
+            double c1 = p0 + p1;                                        /* cumsum */
+            int ch = ((p0 / c1) <= u01(r[2], r[3])) ? 1 : 0;            /* cdf/=cdf[-1]; searchsorted right */
+            if (t + tau > max_time) break;                              /* :65-66 */
+            t = t + tau;                                                /* :68 */
+            if (ch == 0) { S -= 1.0; I += 1.0; } else { I -= 1.0; R += 1.0; }   /* :43-46, :69-70 */
+            ++nev;
+        }
+        x[0] = S; x[1] = I; x[2] = R;
+    } else if (m->model == M_SEIR) {
+        const double beta = m->theta[0], alpha = m->theta[1], gamma = m->theta[2];   /* :92 */
+        double S = x[0], E = x[1], I = x[2], R = x[3];
+        const double N = ((S + E) + I) + R;                             /* :104 */
+        while (E > 0.0 || I > 0.0) {                                    /* :119 */
+            double a0 = ((beta * S) * I) / N, a1 = alpha * E, a2 = gamma * I;   /* :107-109 */
+            double as = (a0 + a1) + a2;
+            philox(k++, j, ptag, f, key, r);
+            double tau = (1.0 / as) * (-log(1.0 - u01(r[0], r[1])));    /* :133 */
+            double p0 = a0 / as, p1 = a1 / as, p2 = a2 / as;
+            double c0 = p0, c1 = c0 + p1, c2 = c1 + p2;
+            double u = u01(r[2], r[3]);
+            int ch = ((c0 / c2) <= u ? 1 : 0) + ((c1 / c2) <= u ? 1 : 0);   /* :134 */
+            if (t + tau > max_time) break;                              /* :136-137 */
+            t = t + tau;
+            if (ch == 0) { S -= 1.0; E += 1.0; }
+            else if (ch == 1) { E -= 1.0; I += 1.0; }
+            else { I -= 1.0; R += 1.0; }                                /* :113-117 */
+            ++nev;
+        }
+        x[0] = S; x[1] = E; x[2] = I; x[3] = R;
+    } else {
+        const int G = m->G, nch = G * G + G;
+        const double gamma = m->theta[G * G];
+        double S[MAXG], I[MAXG], R[MAXG], a[MAXCH], cdf[MAXCH];
+        double sumN = 0.0;
+        for (int g = 0; g < G; ++g) {
+            S[g] = x[3 * g]; I[g] = x[3 * g + 1]; R[g] = x[3 * g + 2];
+            sumN = sumN + ((S[g] + I[g]) + R[g]);                       /* N = [sum(pop[g])], sum(N): :176,:182 */
+        }
+        double infected = 0.0;
+        for (int g = 0; g < G; ++g) infected = infected + I[g];         /* :192 */
+        while (infected > 0.0) {                                        /* :193 */
+            int c = 0;
+            for (int g = 0; g < G; ++g) {                               /* channel order, :180-185 */
+                for (int g2 = 0; g2 < G; ++g2) a[c++] = ((m->theta[g * G + g2] * S[g2]) * I[g]) / sumN;
+                a[c++] = gamma * I[g];
+            }
+            double as = 0.0;
+            for (int i = 0; i < nch; ++i) as = as + a[i];               /* sum(list(values)) :208 */
+            philox(k++, j, ptag, f, key, r);
+            double tau = (1.0 / as) * (-log(1.0 - u01(r[0], r[1])));
+            double run = 0.0;
+            for (int i = 0; i < nch; ++i) { double pi = a[i] / as; run = (i == 0) ? pi : run + pi; cdf[i] = run; }
+            double u = u01(r[2], r[3]);
+            int ch = 0;
+            for (int i = 0; i < nch; ++i) ch += ((cdf[i] / cdf[nch - 1]) <= u) ? 1 : 0;   /* :209-212 */
+            if (t + tau > max_time) break;                              /* :215-216 */
+            t = t + tau;
+            int g = ch / (G + 1), w = ch % (G + 1);
+            if (w < G) { S[w] -= 1.0; I[w] += 1.0; }                    /* s_{g}_{g2}: S_g2 -> I_g2, :183 */
+            else { I[g] -= 1.0; R[g] += 1.0; }                          /* i_{g}: I_g -> R_g, :185 */
+            ++nev;
+            infected = 0.0;
+            for (int q = 0; q < G; ++q) infected = infected + I[q];     /* :222 */
+        }
+        for (int g = 0; g < G; ++g) { x[3 * g] = S[g]; x[3 * g + 1] = I[g]; x[3 * g + 2] = R[g]; }
+    }
+    return nev;
+}
+
+static int load_model(model_t* m, int model, int G, const double* theta, int d) {
+    memset(m, 0, sizeof *m);
+    m->model = model;
+    m->G = (model >= M_SUBGROUPS) ? G : 1;
+    m->C = (model == M_SIR) ? 3 : (model == M_SEIR) ? 4 : 3 * G;
+    int need = (model == M_SIR) ? 2 : (model == M_SEIR) ? 3 : G * G + 1;
+    if (model < 0 || model > 3 || d != need || m->G < 1 || m->G > MAXG) return -1;
+    for (int i = 0; i < d; ++i) m->theta[i] = theta[i];
+    return 0;
+}
+
+/* Batched SSA from given states (the per-particle calls of pmcmc.py:201-220, or direct callers). */
+int oracle_simulate(int model, int G, int n, const int32_t* states_in, const double* theta, int d,
+                    double max_time, uint64_t key, uint32_t f, uint32_t step, int32_t* states_out,
+                    int64_t* events_out) {
+    model_t m;
+    if (load_model(&m, model, G, theta, d)) return -1;
+    const uint32_t ptag = (step & 0xFFFFFFu) | ((uint32_t)DOM_SSA << 24);
+    long total = 0;
+#pragma omp parallel for schedule(dynamic, 16) reduction(+ : total)
+    for (int j = 0; j < n; ++j) {
+        double x[MAXC];
+        for (int c = 0; c < m.C; ++c) x[c] = (double)states_in[(size_t)j * m.C + c];
+        total += ssa(&m, x, max_time, key, f, ptag, (uint32_t)j);
+        for (int c = 0; c < m.C; ++c) states_out[(size_t)j * m.C + c] = (int32_t)x[c];
+    }
+    if (events_out) *events_out = total;
+    return 0;
+}
+
+/* ------------------------------------------------------------------ observation weights, pmcmc.py:178-181 */
+static double binom_pmf(double k, double n, double p, double logp, double log1mp) {
+    if (!(p >= 0.0 && p <= 1.0)) return NAN;                   /* scipy _argcheck -> nan */
+    if (k < 0.0 || k > n || k != floor(k)) return 0.0;         /* outside support / non-integral k */
+    if (p == 0.0) return (k == 0.0) ? 1.0 : 0.0;
+    if (p == 1.0) return (k == n) ? 1.0 : 0.0;
+    double a = lgamma(n + 1.0) - lgamma(k + 1.0);
+    a = a - lgamma((n - k) + 1.0);
+    double b = k * logp;
+    double c = (n - k) * log1mp;
+    return exp(a + (b + c));
+}
+static double norm_pdf(double y, double x, double probs) {
+    double scale = probs * x + 0.0001;                         /* pmcmc.py:181 */
+    if (!(scale > 0.0)) return NAN;
+    double z = (y - x) / scale;
+    return (exp(-(z * z) / 2.0) / 2.5066282746310002) / scale;
+}
+/* min over observed columns of the per-column likelihood (np.min propagates NaN) */
+static double weight(int obs, const double* yrow, const double* xobs, int K, double probs, double logp,
+                     double log1mp) {
+    double w = 0.0;
+    for (int i = 0; i < K; ++i) {
+        double wi = (obs == OBS_BINOMIAL) ? binom_pmf(yrow[i], xobs[i], probs, logp, log1mp)
+                                          : norm_pdf(yrow[i], xobs[i], probs);
+        if (i == 0 || isnan(wi)) w = wi;
+        else if (!isnan(w) && wi < w) w = wi;
+    }
+    return w;
+}
+
+/* numpy legacy choice(range(N), N, p=w/sum(w)) given the uniforms, pmcmc.py:185-190.
+ * Returns 0, or 1 when numpy would raise ValueError (NaN probabilities / zero total). */
+int oracle_resample(int n, const double* w, const double* u, int32_t* out) {
+    double S = 0.0;
+    for (int i = 0; i < n; ++i) S = S + w[i];                  /* builtin sum (sequential), :185 */
+    if (!(S > 0.0) || isinf(S)) return 1;
+    double* cdf = (double*)malloc(sizeof(double) * (size_t)n);
+    double c = 0.0;
+    for (int i = 0; i < n; ++i) { double q = w[i] / S; c = (i == 0) ? q : c + q; cdf[i] = c; }   /* cumsum */
+    const double last = cdf[n - 1];
+    for (int i = 0; i < n; ++i) cdf[i] = cdf[i] / last;       /* cdf /= cdf[-1] */
+    for (int j = 0; j < n; ++j) {                              /* searchsorted(u, 'right') */
+        int lo = 0, hi = n;
+        while (lo < hi) { int mid = (lo + hi) >> 1; if (cdf[mid] <= u[j]) lo = mid + 1; else hi = mid; }
+        out[j] = lo;
+    }
+    free(cdf);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ the particle filter, pmcmc.py:123-233
+ * Y [T*K] row-major; theta [d]; npop/mu [G] (G=1 for SIR/SEIR).
+ * Outputs: log_zeta [T] (log of the reference's zetas), zeta [T] (the reference's linear running product),
+ * hidden [T*N*C], ancestry [T*N] (row 0 zeros).  Returns 0 ok, 1 degenerate (reference returns None), <0 bad args. */
+int oracle_particle_filter(int model, int G, int N, int T, int K, const double* Y, const double* theta, int d,
+                           int obs, double probs, const double* npop, const double* mu, uint64_t key, uint32_t f,
+                           int resample_mode, double* log_zeta, double* zeta, int32_t* hidden, int32_t* ancestry,
+                           int64_t* events_out) {
+    model_t m;
+    if (load_model(&m, model, G, theta, d) || N < 1 || T < 1) return -1;
+    const int C = m.C, Gm = m.G;
+    const int Kexp = (model == M_SUBGROUPS2) ? 3 : C;
+    if (K != Kexp) return -1;
+    double* w = (double*)malloc(sizeof(double) * (size_t)N);
+    double* u = (double*)malloc(sizeof(double) * (size_t)N);
+    int32_t* anc = (int32_t*)malloc(sizeof(int32_t) * (size_t)N);
+    const double logp = log(probs), log1mp = log1p(-probs);
+    long total_events = 0;
+    int status = 0;
+    uint32_t r[4];
+
+    /* initial states, :156-170 (Poisson draws by inversion on the keyed stream) */
+    for (int g = 0; g < Gm; ++g) {
+        const double emu = exp(-mu[g]);
+        const int kmax = (int)ceil(mu[g] + 40.0 * sqrt(mu[g]) + 60.0);
+        for (int j = 0; j < N; ++j) {
+            philox((uint32_t)g, (uint32_t)j, (uint32_t)DOM_INIT << 24, f, key, r);
+            double U = u01(r[0], r[1]), pk = emu, F = pk;
+            int k = 0;
+            while (U >= F && k < kmax) { k += 1; pk = pk * mu[g] / (double)k; F = F + pk; }
+            int32_t* x = hidden + (size_t)j * C;
+            if (model == M_SIR) { x[1] = k; x[0] = (int32_t)(npop[0] - k); x[2] = 0; }
+            else if (model == M_SEIR) { x[2] = k; x[0] = (int32_t)(npop[0] - k); x[1] = 0; x[3] = 0; }
+            else { x[3 * g + 1] = k; x[3 * g] = (int32_t)(npop[g] - k); x[3 * g + 2] = 0; }
+        }
+    }
+    for (int j = 0; j < N; ++j) ancestry[j] = 0;
+    log_zeta[0] = 0.0;
+    zeta[0] = 1.0;
+
+    for (int p = 1; p < T; ++p) {
+        const int32_t* prev = hidden + (size_t)(p - 1) * N * C;
+        int32_t* cur = hidden + (size_t)p * N * C;
+        /* (a) weights from state p-1 against Y[p-1], :178-181 */
+        for (int j = 0; j < N; ++j) {
+            double xo[MAXC];
+            if (model == M_SUBGROUPS2) {
+                for (int c = 0; c < 3; ++c) { double s = 0.0; for (int g = 0; g < Gm; ++g) s = s + prev[(size_t)j * C + 3 * g + c]; xo[c] = s; }
+            } else {
+                for (int c = 0; c < C; ++c) xo[c] = prev[(size_t)j * C + c];
+            }
+            w[j] = weight(obs, Y + (size_t)(p - 1) * K, xo, K, probs, logp, log1mp);
+        }
+        /* (b) zetas[p] = zetas[p-1] * mean(w), :183 */
+        double sw = 0.0;
+        for (int j = 0; j < N; ++j) sw = sw + w[j];
+        const double mean = sw / (double)N;
+        zeta[p] = zeta[p - 1] * mean;
+        log_zeta[p] = log_zeta[p - 1] + log(mean);
+        /* (c,d,e) normalise + resample, :185-193 */
+        if (resample_mode == RS_SYSTEMATIC) {
+            philox(0, 0, ((uint32_t)p & 0xFFFFFFu) | ((uint32_t)DOM_RESAMPLE << 24), f, key, r);
+            double U = u01(r[0], r[1]);
+            for (int j = 0; j < N; ++j) u[j] = ((double)j + U) / (double)N;
+        } else {
+            for (int j = 0; j < N; ++j) {
+                philox(0, (uint32_t)j, ((uint32_t)p & 0xFFFFFFu) | ((uint32_t)DOM_RESAMPLE << 24), f, key, r);
+                u[j] = u01(r[0], r[1]);
+            }
+        }
+        if (oracle_resample(N, w, u, anc)) { status = 1; break; }   /* ValueError -> (None, None, None), :191-192 */
+        for (int j = 0; j < N; ++j) ancestry[(size_t)p * N + j] = anc[j];
+        /* (f,g,h) gather parents and propagate over [0, 1], :195-231 */
+        const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | ((uint32_t)DOM_SSA << 24);
+        long ev = 0;
+#pragma omp parallel for schedule(dynamic, 16) reduction(+ : ev)
+        for (int j = 0; j < N; ++j) {
+            double x[MAXC];
+            for (int c = 0; c < C; ++c) x[c] = (double)prev[(size_t)anc[j] * C + c];
+            ev += ssa(&m, x, 1.0, key, f, ptag, (uint32_t)j);
+            for (int c = 0; c < C; ++c) cur[(size_t)j * C + c] = (int32_t)x[c];
+        }
+        total_events += ev;
+    }
+    if (events_out) *events_out = total_events;
+    free(w); free(u); free(anc);
+    return status;
+}
+
+int oracle_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+/* scalar weight functions, exported so tests can pin them against scipy (tests/golden/kernels_golden.npz) */
+double oracle_binom_pmf(double k, double n, double p) { return binom_pmf(k, n, p, log(p), log1p(-p)); }
+double oracle_norm_pdf(double y, double x, double probs) { return norm_pdf(y, x, probs); }

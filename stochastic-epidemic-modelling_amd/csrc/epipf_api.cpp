@@ -1,0 +1,460 @@
+// epipf_api.cpp -- the C ABI of libepipf.so (declared in include/epipf.h).
+//
+// A context owns every device buffer for one (model, G, N, t_max, max_chains) shape and one HIP
+// stream; the observations, the log-factorial table and the whole particle history stay resident in
+// HBM across calls, so an MH iteration moves only the chain parameters (host->device, ~200 B per
+// chain) and the log-likelihoods + status (device->host) over PCIe.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../../include/epipf.h"
+#include "epipf_internal.hpp"
+
+using namespace epipf;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                   \
+    do {                                                                                                \
+        hipError_t e_ = (expr);                                                                         \
+        if (e_ != hipSuccess) return fail(EPIPF_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));   \
+    } while (0)
+
+template <class T>
+int dalloc(T** p, size_t n) {
+    if (n == 0) n = 1;
+    if (hipMalloc((void**)p, n * sizeof(T)) != hipSuccess) {
+        *p = nullptr;
+        return fail(EPIPF_ENOMEM, "hipMalloc of %zu bytes failed", n * sizeof(T));
+    }
+    return 0;
+}
+
+int default_wg(int N) {
+    const char* e = getenv("EPIPF_WG");
+    if (e) {
+        int v = atoi(e);
+        if (v == 64 || v == 256) return v;
+    }
+    (void)N;
+    return 64;
+}
+}  // namespace
+
+struct epipf_ctx {
+    int device = 0, model = 0, G = 1, C = 3, K = 3, N = 0, Tmax = 0, max_chains = 0, wg = 64, B = 0;
+    hipStream_t stream = nullptr;
+    size_t hist_stride = 0, anc_stride = 0, wstride = 0, bstride = 0;
+    int32_t *hidden = nullptr, *ancestry = nullptr, *status = nullptr, *chosen = nullptr, *traj = nullptr;
+    double *wraw = nullptr, *wloc = nullptr, *bsum = nullptr, *log_zeta = nullptr, *Y = nullptr, *lf = nullptr;
+    ChainParam* cp = nullptr;
+    unsigned long long* counters = nullptr;
+    // pinned staging
+    ChainParam* h_cp = nullptr;
+    int32_t* h_status = nullptr;
+    double* h_lz = nullptr;
+    unsigned long long* h_counters = nullptr;
+    int T = 0, lf_max = -1, lf_cap = 0, last_chains = 0, last_T = 0;
+    bool have_Y = false, have_pop = false, have_run = false, profiling = false;
+    double npop[kMaxG] = {0}, mu[kMaxG] = {0}, emu[kMaxG] = {0};
+    int kmax[kMaxG] = {0};
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    epipf_stats stats{};
+    // scratch for epipf_simulate / epipf_resample (grown on demand)
+    size_t scratch_bytes = 0;
+    void* scratch = nullptr;
+};
+
+static int theta_dim(int model, int G) { return model == EPIPF_SIR ? 2 : model == EPIPF_SEIR ? 3 : G * G + 1; }
+
+static void free_ctx(epipf_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    void* dev[] = {c->hidden, c->ancestry, c->status, c->chosen, c->traj, c->wraw, c->wloc, c->bsum,
+                   c->log_zeta, c->Y, c->lf, c->cp, c->counters, c->scratch};
+    for (void* p : dev)
+        if (p) (void)hipFree(p);
+    void* host[] = {c->h_cp, c->h_status, c->h_lz, c->h_counters};
+    for (void* p : host)
+        if (p) (void)hipHostFree(p);
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" {
+
+const char* epipf_last_error(void) { return g_err.c_str(); }
+int epipf_abi_version(void) { return EPIPF_ABI_VERSION; }
+int epipf_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_particles, int t_max, int max_chains) {
+    if (!out) return fail(EPIPF_EINVAL, "out is NULL");
+    *out = nullptr;
+    if (model < EPIPF_SIR || model > EPIPF_SIR_SUBGROUPS2) return fail(EPIPF_EINVAL, "unknown model %d", model);
+    const int G = model >= EPIPF_SIR_SUBGROUPS ? groups : 1;
+    if (G < 1 || G > kMaxG) return fail(EPIPF_EINVAL, "groups must be in [1, %d], got %d", kMaxG, groups);
+    if (n_particles < 1 || t_max < 1 || max_chains < 1) return fail(EPIPF_EINVAL, "n_particles, t_max, max_chains must be >= 1");
+    if (t_max > (1 << 24)) return fail(EPIPF_EINVAL, "t_max must be < 2^24 (Philox step field)");
+    int ndev = epipf_device_count();
+    if (device < 0 || device >= ndev) return fail(EPIPF_EINVAL, "device %d not present (%d HIP devices)", device, ndev);
+    epipf_ctx* c = new epipf_ctx();
+    c->device = device;
+    c->model = model;
+    c->G = G;
+    c->C = model == EPIPF_SIR ? 3 : model == EPIPF_SEIR ? 4 : 3 * G;
+    c->K = model == EPIPF_SIR_SUBGROUPS2 ? 3 : c->C;
+    c->N = n_particles;
+    c->Tmax = t_max;
+    c->max_chains = max_chains;
+    c->wg = default_wg(n_particles);
+    c->B = (n_particles + c->wg - 1) / c->wg;
+    if (step_lds_bytes(c->B, c->wg) > 160 * 1024) {
+        free_ctx(c);
+        return fail(EPIPF_EINVAL, "n_particles %d too large for one LDS block-sum table", n_particles);
+    }
+    c->hist_stride = (size_t)t_max * n_particles * c->C;
+    c->anc_stride = (size_t)t_max * n_particles;
+    c->wstride = (size_t)c->B * c->wg;
+    c->bstride = (size_t)c->B;
+    int rc = 0;
+    if (hipSetDevice(device) != hipSuccess) { free_ctx(c); return fail(EPIPF_EHIP, "hipSetDevice(%d) failed", device); }
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        free_ctx(c);
+        return fail(EPIPF_EHIP, "hipStreamCreate failed");
+    }
+    rc |= dalloc(&c->hidden, (size_t)max_chains * c->hist_stride);
+    rc |= dalloc(&c->ancestry, (size_t)max_chains * c->anc_stride);
+    rc |= dalloc(&c->status, (size_t)max_chains);
+    rc |= dalloc(&c->chosen, (size_t)max_chains);
+    rc |= dalloc(&c->traj, (size_t)max_chains * t_max * c->C);
+    rc |= dalloc(&c->wraw, 2 * (size_t)max_chains * c->wstride);
+    rc |= dalloc(&c->wloc, 2 * (size_t)max_chains * c->wstride);
+    rc |= dalloc(&c->bsum, 2 * (size_t)max_chains * c->bstride);
+    rc |= dalloc(&c->log_zeta, (size_t)max_chains * t_max);
+    rc |= dalloc(&c->cp, (size_t)max_chains);
+    rc |= dalloc(&c->counters, 4);
+    if (rc) { free_ctx(c); return EPIPF_ENOMEM; }
+    if (hipHostMalloc((void**)&c->h_cp, sizeof(ChainParam) * max_chains) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_status, sizeof(int32_t) * max_chains) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_lz, sizeof(double) * (size_t)max_chains * t_max) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_counters, sizeof(unsigned long long) * 4) != hipSuccess) {
+        free_ctx(c);
+        return fail(EPIPF_ENOMEM, "hipHostMalloc failed");
+    }
+    for (auto& e : c->ev)
+        if (hipEventCreate(&e) != hipSuccess) { free_ctx(c); return fail(EPIPF_EHIP, "hipEventCreate failed"); }
+    if (hipMemsetAsync(c->counters, 0, 4 * sizeof(unsigned long long), c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+        free_ctx(c);
+        return fail(EPIPF_EHIP, "counter init failed");
+    }
+    *out = c;
+    return EPIPF_OK;
+}
+
+void epipf_destroy(epipf_ctx* ctx) { free_ctx(ctx); }
+
+int epipf_set_observations(epipf_ctx* c, const double* Y, int T, int K) {
+    if (!c || !Y) return fail(EPIPF_EINVAL, "NULL argument");
+    if (T < 1 || T > c->Tmax) return fail(EPIPF_EINVAL, "T=%d outside [1, t_max=%d]", T, c->Tmax);
+    if (K != c->K) return fail(EPIPF_EINVAL, "K=%d but the model observes %d columns", K, c->K);
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->Y) { HIP_TRY(hipStreamSynchronize(c->stream)); (void)hipFree(c->Y); c->Y = nullptr; }
+    if (dalloc(&c->Y, (size_t)T * K)) return EPIPF_ENOMEM;
+    HIP_TRY(hipMemcpyAsync(c->Y, Y, sizeof(double) * (size_t)T * K, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->T = T;
+    c->have_Y = true;
+    return EPIPF_OK;
+}
+
+int epipf_set_population(epipf_ctx* c, const double* n_population, const double* mu) {
+    if (!c || !n_population || !mu) return fail(EPIPF_EINVAL, "NULL argument");
+    double tot = 0.0;
+    for (int g = 0; g < c->G; ++g) {
+        const double np_ = n_population[g], m = mu[g];
+        if (!(np_ >= 0.0) || np_ != std::floor(np_) || np_ > 1e8)
+            return fail(EPIPF_EINVAL, "n_population[%d]=%g must be an integer in [0, 1e8]", g, np_);
+        if (!(m >= 0.0) || m > 700.0) return fail(EPIPF_EINVAL, "mu[%d]=%g must be in [0, 700]", g, m);
+        c->npop[g] = np_;
+        c->mu[g] = m;
+        c->emu[g] = std::exp(-m);                                        // host glibc, as the oracle
+        c->kmax[g] = (int)std::ceil(m + 40.0 * std::sqrt(m) + 60.0);
+        tot += np_;
+    }
+    const int need = (int)tot;
+    HIP_TRY(hipSetDevice(c->device));
+    if (need + 1 > c->lf_cap) {
+        if (c->lf) { HIP_TRY(hipStreamSynchronize(c->stream)); (void)hipFree(c->lf); c->lf = nullptr; }
+        if (dalloc(&c->lf, (size_t)need + 1)) return EPIPF_ENOMEM;
+        c->lf_cap = need + 1;
+    }
+    if (need != c->lf_max) {
+        std::vector<double> lf((size_t)need + 1);
+        for (int n = 0; n <= need; ++n) lf[n] = std::lgamma((double)n + 1.0);   // scipy binom.pmf restatement
+        HIP_TRY(hipMemcpyAsync(c->lf, lf.data(), sizeof(double) * lf.size(), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        c->lf_max = need;
+    }
+    c->have_pop = true;
+    return EPIPF_OK;
+}
+
+int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_model, const double* probs,
+              const uint64_t* keys, const uint32_t* filter_index, const int32_t* active, int resample_mode,
+              double* log_zetas_out, int32_t* status_out) {
+    if (!c || !theta || !probs || !keys || !filter_index || !status_out) return fail(EPIPF_EINVAL, "NULL argument");
+    if (!c->have_Y) return fail(EPIPF_ESTATE, "epipf_set_observations was not called");
+    if (!c->have_pop) return fail(EPIPF_ESTATE, "epipf_set_population was not called");
+    if (n_chains < 1 || n_chains > c->max_chains) return fail(EPIPF_EINVAL, "n_chains=%d outside [1, %d]", n_chains, c->max_chains);
+    if (d != theta_dim(c->model, c->G)) return fail(EPIPF_EINVAL, "theta has %d entries per chain, model needs %d", d, theta_dim(c->model, c->G));
+    if (obs_model != EPIPF_OBS_BINOMIAL && obs_model != EPIPF_OBS_NORMAL) return fail(EPIPF_EINVAL, "bad obs_model %d", obs_model);
+    if (resample_mode != EPIPF_RESAMPLE_MULTINOMIAL && resample_mode != EPIPF_RESAMPLE_SYSTEMATIC)
+        return fail(EPIPF_EINVAL, "bad resample_mode %d", resample_mode);
+    int n_active = 0;
+    for (int ch = 0; ch < n_chains; ++ch) {
+        const bool on = !active || active[ch];
+        ChainParam& q = c->h_cp[ch];
+        memset(&q, 0, sizeof q);
+        for (int i = 0; i < d; ++i) {
+            const double v = theta[(size_t)ch * d + i];
+            if (on && !(v >= 0.0 && v < INFINITY))
+                return fail(EPIPF_EINVAL, "theta[%d][%d]=%g: parameters must be finite and >= 0 (pmcmc.py:333)", ch, i, v);
+            q.theta[i] = v;
+        }
+        q.probs = probs[ch];
+        q.logp = std::log(probs[ch]);
+        q.log1mp = std::log1p(-probs[ch]);
+        q.k0 = (uint32_t)keys[ch];
+        q.k1 = (uint32_t)(keys[ch] >> 32);
+        q.f = filter_index[ch];
+        c->h_status[ch] = on ? EPIPF_STATUS_OK : EPIPF_STATUS_SKIPPED;
+        n_active += on;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpyAsync(c->cp, c->h_cp, sizeof(ChainParam) * n_chains, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->status, c->h_status, sizeof(int32_t) * n_chains, hipMemcpyHostToDevice, c->stream));
+
+    StepArgs a{};
+    a.N = c->N; a.T = c->T; a.B = c->B; a.wg = c->wg; a.max_chains = c->max_chains;
+    a.resample_mode = resample_mode; a.count_events = c->profiling ? 1 : 0; a.lf_max = c->lf_max;
+    a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride; a.wstride = c->wstride; a.bstride = c->bstride;
+    a.delta = (8.0 * (double)c->N + 256.0) * 0x1.0p-53;
+    a.Y = c->Y; a.lf = c->lf; a.cp = c->cp; a.hidden = c->hidden; a.ancestry = c->ancestry;
+    a.wraw = c->wraw; a.wloc = c->wloc; a.bsum = c->bsum; a.log_zeta = c->log_zeta; a.status = c->status;
+    a.counters = c->counters;
+    for (int g = 0; g < kMaxG; ++g) { a.npop[g] = c->npop[g]; a.mu[g] = c->mu[g]; a.emu[g] = c->emu[g]; a.kmax[g] = c->kmax[g]; }
+
+    hipEvent_t e0 = c->profiling ? c->ev[0] : nullptr, e1 = c->profiling ? c->ev[1] : nullptr,
+               e2 = c->profiling ? c->ev[2] : nullptr;
+    hipError_t le = launch_filter(a, c->model, c->G, obs_model, n_chains, c->stream, e0, e1, e2);
+    if (le != hipSuccess) return fail(EPIPF_EHIP, "kernel launch failed: %s", hipGetErrorString(le));
+    HIP_TRY(hipMemcpyAsync(c->h_status, c->status, sizeof(int32_t) * n_chains, hipMemcpyDeviceToHost, c->stream));
+    if (log_zetas_out)
+        HIP_TRY(hipMemcpyAsync(c->h_lz, c->log_zeta, sizeof(double) * (size_t)n_chains * c->T, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_counters, c->counters, sizeof(unsigned long long) * 2, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    memcpy(status_out, c->h_status, sizeof(int32_t) * n_chains);
+    if (log_zetas_out) {
+        memcpy(log_zetas_out, c->h_lz, sizeof(double) * (size_t)n_chains * c->T);
+        // steps after a degenerate step were never run: report -inf there (zetas = 0)
+        for (int ch = 0; ch < n_chains; ++ch) {
+            if (c->h_status[ch] == EPIPF_STATUS_OK) continue;
+            bool dead = false;
+            for (int p = 0; p < c->T; ++p) {
+                double& v = log_zetas_out[(size_t)ch * c->T + p];
+                if (c->h_status[ch] == EPIPF_STATUS_SKIPPED) { v = NAN; continue; }
+                if (dead) v = -INFINITY;
+                else if (v == -INFINITY) dead = true;
+            }
+        }
+    }
+    if (c->profiling) {
+        float ms_init = 0.f, ms_step = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms_init, c->ev[0], c->ev[1]));
+        HIP_TRY(hipEventElapsedTime(&ms_step, c->ev[1], c->ev[2]));
+        c->stats.init_ms += ms_init;
+        c->stats.init_launches += 1;
+        c->stats.step_ms += ms_step;
+        c->stats.step_launches += c->T - 1;
+    }
+    c->stats.events = (int64_t)c->h_counters[0];
+    c->stats.resample_fallbacks = (int64_t)c->h_counters[1];
+    c->stats.particle_steps += (int64_t)n_active * c->N * c->T;
+    c->stats.filters += n_active;
+    c->last_chains = n_chains;
+    c->last_T = c->T;
+    c->have_run = true;
+    return EPIPF_OK;
+}
+
+int epipf_copy_history(epipf_ctx* c, int n_chains, int32_t* hidden_out, int32_t* ancestry_out) {
+    if (!c) return fail(EPIPF_EINVAL, "NULL context");
+    if (!c->have_run) return fail(EPIPF_ESTATE, "no filter has run on this context");
+    if (n_chains < 1 || n_chains > c->last_chains) return fail(EPIPF_EINVAL, "n_chains=%d outside [1, %d]", n_chains, c->last_chains);
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t T = (size_t)c->last_T;
+    if (hidden_out)
+        HIP_TRY(hipMemcpy2DAsync(hidden_out, T * c->N * c->C * sizeof(int32_t), c->hidden, c->hist_stride * sizeof(int32_t),
+                                 T * c->N * c->C * sizeof(int32_t), n_chains, hipMemcpyDeviceToHost, c->stream));
+    if (ancestry_out)
+        HIP_TRY(hipMemcpy2DAsync(ancestry_out, T * c->N * sizeof(int32_t), c->ancestry, c->anc_stride * sizeof(int32_t),
+                                 T * c->N * sizeof(int32_t), n_chains, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return EPIPF_OK;
+}
+
+int epipf_path_sample(epipf_ctx* c, int n_chains, const int32_t* chosen, int32_t* traj_out) {
+    if (!c || !chosen || !traj_out) return fail(EPIPF_EINVAL, "NULL argument");
+    if (!c->have_run) return fail(EPIPF_ESTATE, "no filter has run on this context");
+    if (n_chains < 1 || n_chains > c->last_chains) return fail(EPIPF_EINVAL, "n_chains=%d outside [1, %d]", n_chains, c->last_chains);
+    for (int ch = 0; ch < n_chains; ++ch)
+        if (chosen[ch] < 0 || chosen[ch] >= c->N) return fail(EPIPF_EINVAL, "chosen[%d]=%d outside [0, N)", ch, chosen[ch]);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpyAsync(c->chosen, chosen, sizeof(int32_t) * n_chains, hipMemcpyHostToDevice, c->stream));
+    PathArgs a{};
+    a.n_chains = n_chains; a.N = c->N; a.T = c->last_T; a.C = c->C;
+    a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride;
+    a.hidden = c->hidden; a.ancestry = c->ancestry; a.chosen = c->chosen; a.traj = c->traj;
+    hipError_t le = launch_path_sample(a, c->stream);
+    if (le != hipSuccess) return fail(EPIPF_EHIP, "path kernel launch failed: %s", hipGetErrorString(le));
+    HIP_TRY(hipMemcpyAsync(traj_out, c->traj, sizeof(int32_t) * (size_t)n_chains * a.T * a.C, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return EPIPF_OK;
+}
+
+static int ensure_scratch(epipf_ctx* c, size_t bytes) {
+    if (bytes <= c->scratch_bytes) return 0;
+    if (c->scratch) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->scratch); c->scratch = nullptr; c->scratch_bytes = 0; }
+    if (hipMalloc(&c->scratch, bytes) != hipSuccess) return fail(EPIPF_ENOMEM, "scratch hipMalloc(%zu) failed", bytes);
+    c->scratch_bytes = bytes;
+    return 0;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int epipf_simulate(epipf_ctx* c, int n, const int32_t* states_in, const double* theta, int d, double max_time,
+                   uint64_t key, uint32_t filter_index, uint32_t step, int32_t* states_out, int64_t* events_out) {
+    if (!c || !states_in || !theta || !states_out) return fail(EPIPF_EINVAL, "NULL argument");
+    if (n < 0) return fail(EPIPF_EINVAL, "n < 0");
+    if (d != theta_dim(c->model, c->G)) return fail(EPIPF_EINVAL, "theta needs %d entries", theta_dim(c->model, c->G));
+    if (!(max_time >= 0.0)) return fail(EPIPF_EINVAL, "max_time must be >= 0");
+    for (int i = 0; i < d; ++i)
+        if (!(theta[i] >= 0.0 && theta[i] < INFINITY)) return fail(EPIPF_EINVAL, "theta[%d] must be finite and >= 0", i);
+    for (size_t i = 0; i < (size_t)n * c->C; ++i)
+        if (states_in[i] < 0) return fail(EPIPF_EINVAL, "states must be non-negative");
+    if (n == 0) { if (events_out) *events_out = 0; return EPIPF_OK; }
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t sb = align256((size_t)n * c->C * sizeof(int32_t));
+    const size_t need = align256(sizeof(ChainParam)) + 2 * sb + 256;
+    if (ensure_scratch(c, need)) return EPIPF_ENOMEM;
+    char* base = (char*)c->scratch;
+    ChainParam* dcp = (ChainParam*)base;
+    int32_t* din = (int32_t*)(base + align256(sizeof(ChainParam)));
+    int32_t* dout = (int32_t*)((char*)din + sb);
+    unsigned long long* dev_events = (unsigned long long*)((char*)dout + sb);
+    ChainParam q;
+    memset(&q, 0, sizeof q);
+    for (int i = 0; i < d; ++i) q.theta[i] = theta[i];
+    q.k0 = (uint32_t)key; q.k1 = (uint32_t)(key >> 32); q.f = filter_index;
+    HIP_TRY(hipMemcpyAsync(dcp, &q, sizeof q, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(din, states_in, sizeof(int32_t) * (size_t)n * c->C, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(dev_events, 0, sizeof(unsigned long long), c->stream));
+    SimArgs a{};
+    a.n = n; a.step = step; a.tmax = max_time; a.cp = dcp; a.in = din; a.out = dout; a.events = dev_events;
+    hipError_t le = launch_simulate(a, c->model, c->G, c->stream);
+    if (le != hipSuccess) return fail(EPIPF_EHIP, "simulate launch failed: %s", hipGetErrorString(le));
+    unsigned long long ev = 0;
+    HIP_TRY(hipMemcpyAsync(states_out, dout, sizeof(int32_t) * (size_t)n * c->C, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&ev, dev_events, sizeof ev, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (events_out) *events_out = (int64_t)ev;
+    return EPIPF_OK;
+}
+
+int epipf_resample(epipf_ctx* c, int n, const double* w, const double* u, int32_t* out, int64_t* fallbacks_out) {
+    if (!c || !w || !u || !out) return fail(EPIPF_EINVAL, "NULL argument");
+    if (n < 1) return fail(EPIPF_EINVAL, "n must be >= 1");
+    const int B = (n + 255) / 256;
+    if (step_lds_bytes(B, 256) > 160 * 1024) return fail(EPIPF_EINVAL, "n too large");
+    for (int i = 0; i < n; ++i)
+        if (!(u[i] >= 0.0 && u[i] < 1.0)) return fail(EPIPF_EINVAL, "uniforms must lie in [0, 1)");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t nw = align256(sizeof(double) * (size_t)B * 256);
+    const size_t need = 4 * nw + align256(sizeof(double) * B) + align256(sizeof(int32_t) * (size_t)n) + 512;
+    if (ensure_scratch(c, need)) return EPIPF_ENOMEM;
+    char* p = (char*)c->scratch;
+    ResampleArgs a{};
+    a.N = n; a.B = B; a.delta = (8.0 * (double)n + 256.0) * 0x1.0p-53;
+    double* dw = (double*)p; p += nw;
+    double* du = (double*)p; p += nw;
+    a.wraw = (double*)p; p += nw;
+    a.wloc = (double*)p; p += nw;
+    a.bsum = (double*)p; p += align256(sizeof(double) * B);
+    a.out = (int32_t*)p; p += align256(sizeof(int32_t) * (size_t)n);
+    a.status = (int32_t*)p; p += 256;
+    a.fallbacks = (unsigned long long*)p;
+    a.w = dw; a.u = du;
+    HIP_TRY(hipMemcpyAsync(dw, w, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(du, u, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(a.status, 0, 256 + sizeof(unsigned long long), c->stream));
+    hipError_t le = launch_resample(a, c->stream);
+    if (le != hipSuccess) return fail(EPIPF_EHIP, "resample launch failed: %s", hipGetErrorString(le));
+    int32_t st = 0;
+    unsigned long long fb = 0;
+    HIP_TRY(hipMemcpyAsync(out, a.out, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&st, a.status, sizeof st, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&fb, a.fallbacks, sizeof fb, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (fallbacks_out) *fallbacks_out = (int64_t)fb;
+    return st ? EPIPF_STATUS_DEGENERATE : EPIPF_OK;
+}
+
+int epipf_set_profiling(epipf_ctx* c, int enable) {
+    if (!c) return fail(EPIPF_EINVAL, "NULL context");
+    c->profiling = enable != 0;
+    return EPIPF_OK;
+}
+
+int epipf_get_stats(epipf_ctx* c, epipf_stats* out) {
+    if (!c || !out) return fail(EPIPF_EINVAL, "NULL argument");
+    *out = c->stats;
+    return EPIPF_OK;
+}
+
+int epipf_reset_stats(epipf_ctx* c) {
+    if (!c) return fail(EPIPF_EINVAL, "NULL context");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemsetAsync(c->counters, 0, 4 * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    memset(&c->stats, 0, sizeof c->stats);
+    return EPIPF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,291 @@
+// epipf_device.hpp -- device building blocks of the particle filter (gfx950 / CDNA4, wave64).
+//
+// Everything here is compiled with -ffp-contract=off: each IEEE multiply, add and divide must
+// round exactly as CPython/numpy round the reference's expressions, so that Gillespie channel
+// choices, state trajectories and resampled ancestors are bit-identical to the reference driven
+// by the same keyed Philox stream.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace epipf {
+
+constexpr int kMaxG = 4;                    // largest subgroup count instantiated
+constexpr int kMaxC = 3 * kMaxG;            // compartments per particle
+constexpr int kMaxTheta = kMaxG * kMaxG + 1;
+constexpr uint32_t kDomainSSA = 0u << 24;
+constexpr uint32_t kDomainResample = 1u << 24;
+constexpr uint32_t kDomainInit = 2u << 24;
+
+enum Model : int { kSIR = 0, kSEIR = 1, kSubgroups = 2, kSubgroups2 = 3 };
+enum Obs : int { kBinomial = 0, kNormal = 1 };
+
+// ------------------------------------------------------------------------------- Philox4x32-10
+// Salmon et al. SC'11; constants and key schedule of Random123.  Counter words: (c0, c1, c2, c3).
+struct Block { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ Block philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                        uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return Block{c0, c1, c2, c3};
+}
+
+// 53-bit uniform in [0, 1): ((hi << 32 | lo) >> 11) * 2^-53  (numpy's Philox double convention)
+__device__ __forceinline__ double u01(uint32_t lo, uint32_t hi) {
+    const uint64_t v = ((uint64_t)hi << 32) | lo;
+    return (double)(v >> 11) * 0x1.0p-53;
+}
+
+// ------------------------------------------------------------------------------- per-chain parameters
+struct ChainParam {
+    double theta[kMaxTheta];   // SIR: beta,gamma  SEIR: beta,alpha,gamma  groups: beta[G][G], gamma
+    double probs;              // binomial p, or normal noise ratio
+    double logp, log1mp;       // log(p), log1p(-p)  (host glibc, identical to the oracle's)
+    uint32_t k0, k1;           // Philox key
+    uint32_t f;                // filter index
+    uint32_t pad;
+};
+
+// ------------------------------------------------------------------------------- Gillespie SSA
+// Direct method over [0, tmax] from state x (integers held in doubles, as the reference holds them),
+// gillespie_algo.py.  Event k of this lane draws Philox block (k, j, ptag, f): tau from (x,y), the
+// channel from (z,w).  Both uniforms are consumed before the overshoot test, as in the reference.
+template <int MODEL, int G>
+__device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
+                                             double tmax) {
+    double t = 0.0;
+    uint32_t k = 0;
+    int nev = 0;
+    if constexpr (MODEL == kSIR) {
+        const double beta = cp.theta[0], gamma = cp.theta[1];
+        double S = x[0], I = x[1], R = x[2];
+        const double N = (S + I) + R;                                  // gillespie_algo.py:35
+        while (I > 0.0) {                                              // :48
+            const Block r = philox(k, j, ptag, cp.f, cp.k0, cp.k1);
+            ++k;
+            const double a0 = ((beta * S) * I) / N;                    // :38
+            const double a1 = gamma * I;                               // :39
+            const double as = a0 + a1;
+            const double tau = (1.0 / as) * (-log(1.0 - u01(r.x, r.y)));   // np.random.exponential, :62
+            const double p0 = a0 / as, p1 = a1 / as;                   // choice(p=a/sum(a)), :63
+            const bool second = (p0 / (p0 + p1)) <= u01(r.z, r.w);     // cdf/cdf[-1], searchsorted right
+            if (t + tau > tmax) break;                                 // :65-66
+            t = t + tau;
+            if (second) { I -= 1.0; R += 1.0; } else { S -= 1.0; I += 1.0; }
+            ++nev;
+        }
+        x[0] = S; x[1] = I; x[2] = R;
+    } else if constexpr (MODEL == kSEIR) {
+        const double beta = cp.theta[0], alpha = cp.theta[1], gamma = cp.theta[2];   // :92
+        double S = x[0], E = x[1], I = x[2], R = x[3];
+        const double N = ((S + E) + I) + R;                            // :104
+        while (E > 0.0 || I > 0.0) {                                   // :119
+            const Block r = philox(k, j, ptag, cp.f, cp.k0, cp.k1);
+            ++k;
+            const double a0 = ((beta * S) * I) / N, a1 = alpha * E, a2 = gamma * I;
+            const double as = (a0 + a1) + a2;
+            const double tau = (1.0 / as) * (-log(1.0 - u01(r.x, r.y)));   // :133
+            const double p0 = a0 / as, p1 = a1 / as, p2 = a2 / as;
+            const double c1 = p0 + p1, c2 = c1 + p2;
+            const double u = u01(r.z, r.w);
+            const int ch = ((p0 / c2) <= u ? 1 : 0) + ((c1 / c2) <= u ? 1 : 0);   // :134
+            if (t + tau > tmax) break;                                 // :136-137
+            t = t + tau;
+            if (ch == 0) { S -= 1.0; E += 1.0; }
+            else if (ch == 1) { E -= 1.0; I += 1.0; }
+            else { I -= 1.0; R += 1.0; }
+            ++nev;
+        }
+        x[0] = S; x[1] = E; x[2] = I; x[3] = R;
+    } else {
+        constexpr int NCH = G * G + G;
+        const double gamma = cp.theta[G * G];
+        double S[G], I[G], R[G];
+        double sumN = 0.0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            S[g] = x[3 * g]; I[g] = x[3 * g + 1]; R[g] = x[3 * g + 2];
+            sumN = sumN + ((S[g] + I[g]) + R[g]);                      // sum(N), :176,:182
+        }
+        double infected = 0.0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) infected = infected + I[g];        // :192
+        while (infected > 0.0) {                                       // :193
+            const Block r = philox(k, j, ptag, cp.f, cp.k0, cp.k1);
+            ++k;
+            double a[NCH];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {                              // channel order, :180-185
+#pragma unroll
+                for (int g2 = 0; g2 < G; ++g2) a[g * (G + 1) + g2] = ((cp.theta[g * G + g2] * S[g2]) * I[g]) / sumN;
+                a[g * (G + 1) + G] = gamma * I[g];
+            }
+            double as = 0.0;
+#pragma unroll
+            for (int i = 0; i < NCH; ++i) as = as + a[i];              // sum(list(values)), :208
+            const double tau = (1.0 / as) * (-log(1.0 - u01(r.x, r.y)));
+            double cdf[NCH];
+            double run = 0.0;
+#pragma unroll
+            for (int i = 0; i < NCH; ++i) { run = run + a[i] / as; cdf[i] = run; }
+            const double u = u01(r.z, r.w);
+            int ch = 0;
+#pragma unroll
+            for (int i = 0; i < NCH - 1; ++i) ch += ((cdf[i] / cdf[NCH - 1]) <= u) ? 1 : 0;   // :209-212
+            if (t + tau > tmax) break;                                 // :215-216
+            t = t + tau;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+#pragma unroll
+                for (int g2 = 0; g2 < G; ++g2)
+                    if (ch == g * (G + 1) + g2) { S[g2] -= 1.0; I[g2] += 1.0; }   // s_{g}_{g2}: :183
+                if (ch == g * (G + 1) + G) { I[g] -= 1.0; R[g] += 1.0; }         // i_{g}: :185
+            }
+            ++nev;
+            infected = 0.0;
+#pragma unroll
+            for (int g = 0; g < G; ++g) infected = infected + I[g];    // :222
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) { x[3 * g] = S[g]; x[3 * g + 1] = I[g]; x[3 * g + 2] = R[g]; }
+    }
+    return nev;
+}
+
+template <int MODEL, int G>
+struct Shape {
+    static constexpr int C = (MODEL == kSIR) ? 3 : (MODEL == kSEIR) ? 4 : 3 * G;
+    static constexpr int K = (MODEL == kSubgroups2) ? 3 : C;
+};
+
+// ------------------------------------------------------------------------------- observation weights
+// scipy binom.pmf(k, n, p) restated with a host-built log-factorial table lf[n] = lgamma(n + 1),
+// pmcmc.py:179.  Identical expression order to oracle/epipf_oracle.c:binom_pmf.
+__device__ __forceinline__ double binom_pmf(double k, double n, const ChainParam& cp, const double* lf,
+                                            int lf_max) {
+    const double p = cp.probs;
+    if (!(p >= 0.0 && p <= 1.0)) return __builtin_nan("");
+    if (k < 0.0 || k > n || k != floor(k)) return 0.0;
+    if (p == 0.0) return (k == 0.0) ? 1.0 : 0.0;
+    if (p == 1.0) return (k == n) ? 1.0 : 0.0;
+    const int ni = min(max((int)n, 0), lf_max), ki = min(max((int)k, 0), lf_max);
+    double a = lf[ni] - lf[ki];
+    a = a - lf[min(max(ni - ki, 0), lf_max)];
+    const double b = k * cp.logp;
+    const double c = (n - k) * cp.log1mp;
+    return exp(a + (b + c));
+}
+
+// scipy norm.pdf(y, loc=x, scale=probs*x+1e-4), pmcmc.py:181
+__device__ __forceinline__ double normal_pdf(double y, double x, double probs) {
+    const double scale = probs * x + 0.0001;
+    if (!(scale > 0.0)) return __builtin_nan("");
+    const double z = (y - x) / scale;
+    return (exp(-(z * z) / 2.0) / 2.5066282746310002) / scale;
+}
+
+// min over the K observed columns (np.min propagates NaN)
+template <int MODEL, int G, int OBS>
+__device__ __forceinline__ double particle_weight(const double* x, const double* yrow, const ChainParam& cp,
+                                                  const double* lf, int lf_max) {
+    constexpr int K = Shape<MODEL, G>::K;
+    double w = 0.0;
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        double xo;
+        if constexpr (MODEL == kSubgroups2) {
+            xo = 0.0;
+#pragma unroll
+            for (int g = 0; g < G; ++g) xo = xo + x[3 * g + i];       // group sum, pmcmc.py:173,229
+        } else {
+            xo = x[i];
+        }
+        const double wi = (OBS == kBinomial) ? binom_pmf(yrow[i], xo, cp, lf, lf_max) : normal_pdf(yrow[i], xo, cp.probs);
+        if (i == 0 || isnan(wi)) w = wi;
+        else if (!isnan(w) && wi < w) w = wi;
+    }
+    return w;
+}
+
+// ------------------------------------------------------------------------------- block scan (doubles)
+// Inclusive scan of one value per thread across a WG-thread block.  The last thread's result is the
+// block total.  lds must hold WG/64 doubles.  Order of additions is fixed (deterministic).
+template <int WG>
+__device__ __forceinline__ double block_inclusive_scan(double x, double* lds) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double y = __shfl_up(x, o, 64);
+        if (lane >= o) x = x + y;
+    }
+    if constexpr (WG > 64) {
+        if (lane == 63) lds[wave] = x;
+        __syncthreads();
+        double off = 0.0;
+        for (int q = 0; q < wave; ++q) off = off + lds[q];
+        x = off + x;
+        __syncthreads();
+    }
+    return x;
+}
+
+// ------------------------------------------------------------------------------- resampling
+// numpy legacy choice(range(N), N, p=w/sum(w)) for ONE uniform U, exactly (pmcmc.py:185-190):
+//   S = sum(w) (sequential), q = w/S, c = cumsum(q) (sequential), a = #{i : c_i / c_{N-1} <= U}.
+// Used only when the fast parallel search below cannot certify its answer.
+__device__ __noinline__ int resample_exact(double U, const double* w, int N) {
+    double S = 0.0;
+    for (int i = 0; i < N; ++i) S = S + w[i];
+    double c = 0.0;
+    for (int i = 0; i < N; ++i) c = c + w[i] / S;
+    const double last = c;
+    c = 0.0;
+    for (int i = 0; i < N; ++i) {
+        c = c + w[i] / S;
+        if (c / last > U) return i;
+    }
+    return N - 1;
+}
+
+// Two-level search of the parallel CDF v_j = (bpex[b] + wloc[j]) / total (bpex: exclusive prefix of the
+// block sums, in LDS; wloc: in-block inclusive prefix, in HBM/L2).  The answer is certified against
+// the reference's sequential CDF: if v_{a-1} < U - delta and v_a > U + delta, every CDF within delta of
+// v (the sequential one included: delta bounds both roundings) puts U in slot a.
+// Otherwise the draw falls back to resample_exact.
+template <int WG>
+__device__ __forceinline__ int resample_search(double U, const double* bpex, const double* bsum, int B,
+                                               double total, const double* wloc, const double* wraw, int N,
+                                               double delta, bool& fell_back) {
+    int lo = 0, hi = B - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((bpex[mid] + bsum[mid]) / total > U) hi = mid; else lo = mid + 1;
+    }
+    const int b = lo;
+    const double base = bpex[b];
+    const double* L = wloc + (size_t)b * WG;
+    int l = 0, h = WG - 1;
+    while (l < h) {
+        const int m = (l + h) >> 1;
+        if ((base + L[m]) / total > U) h = m; else l = m + 1;
+    }
+    const double va = (base + L[l]) / total;
+    const double vp = (l > 0) ? (base + L[l - 1]) / total
+                              : (b > 0 ? (bpex[b - 1] + bsum[b - 1]) / total : -1.0);
+    int a = b * WG + l;
+    fell_back = false;
+    if (!(va > U + delta) || !(vp < U - delta) || a >= N) {
+        fell_back = true;
+        a = resample_exact(U, wraw, N);
+    }
+    return a;
+}
+
+}  // namespace epipf

@@ -1,0 +1,317 @@
+// epipf_kernels.hip -- the particle-filter kernels for MI355X (gfx950) and their launchers.
+//
+// One filter step (pmcmc.py:177-231) is ONE kernel launch, batched over independent chains
+// (grid.y = chain, grid.x = particle block of WG lanes, one particle per lane):
+//
+//   step p:  [scan of the previous step's block sums in LDS -> total, log-likelihood]
+//            [multinomial draw U_j -> certified two-level CDF search -> ancestor a_j]   (pmcmc.py:183-193)
+//            [gather parent state hidden[p-1][a_j] -> Gillespie SSA over [0,1]]          (pmcmc.py:195-220)
+//            [store hidden[p][j]; weight against Y[p]; in-block scan; block sum]         (pmcmc.py:178-181, next step)
+//
+// so the weights, the in-block CDF and the block sums of step p are produced by the same lanes that
+// produced the states, and the next launch only reads them.  The init kernel draws the Poisson initial
+// states (pmcmc.py:156-175) and the first weights.
+#include "epipf_device.hpp"
+#include "epipf_internal.hpp"
+
+namespace epipf {
+
+// exclusive prefix of the B block sums into LDS (bpex), deterministic order; returns the total.
+template <int WG>
+__device__ __forceinline__ double scan_block_sums(const double* __restrict__ bsum_g, int B, double* bpex,
+                                                  double* bsum, double* red) {
+    const int tid = threadIdx.x;
+    const int per = (B + WG - 1) / WG;
+    const int beg = min(tid * per, B), end = min(beg + per, B);
+    double s = 0.0;
+    for (int i = beg; i < end; ++i) {
+        const double v = bsum_g[i];
+        bsum[i] = v;
+        s = s + v;
+    }
+    const double incl = block_inclusive_scan<WG>(s, red);
+    // exclusive offset of this thread's chunk = inclusive result of the previous thread
+    double* incl_lds = bpex + B;  // scratch after bpex (allocated B + WG)
+    incl_lds[tid] = incl;
+    __syncthreads();
+    double e = (tid == 0) ? 0.0 : incl_lds[tid - 1];
+    for (int i = beg; i < end; ++i) {
+        bpex[i] = e;
+        e = e + bsum[i];
+    }
+    __syncthreads();
+    return bpex[B - 1] + bsum[B - 1];
+}
+
+template <int MODEL, int G, int OBS, int WG>
+__global__ __launch_bounds__(WG) void pf_init_kernel(StepArgs a) {
+    using Sh = Shape<MODEL, G>;
+    constexpr int C = Sh::C;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int chain = blockIdx.y;
+    const int j = blockIdx.x * WG + threadIdx.x;
+    if (a.status[chain] != 0) return;
+    const ChainParam cp = a.cp[chain];
+    double x[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = 0.0;
+    if (j < a.N) {
+#pragma unroll
+        for (int g = 0; g < ((MODEL >= kSubgroups) ? G : 1); ++g) {
+            const Block r = philox((uint32_t)g, (uint32_t)j, kDomainInit, cp.f, cp.k0, cp.k1);
+            const double U = u01(r.x, r.y);
+            const double mu = a.mu[g];
+            double pk = a.emu[g], F = pk;
+            int k = 0;
+            while (U >= F && k < a.kmax[g]) { k += 1; pk = pk * mu / (double)k; F = F + pk; }
+            const double S0 = a.npop[g] - (double)k;
+            if constexpr (MODEL == kSIR) { x[0] = S0; x[1] = (double)k; }
+            else if constexpr (MODEL == kSEIR) { x[0] = S0; x[2] = (double)k; }
+            else { x[3 * g] = S0; x[3 * g + 1] = (double)k; }
+        }
+        int32_t* h = a.hidden + (size_t)chain * a.hist_stride + (size_t)j * C;
+#pragma unroll
+        for (int c = 0; c < C; ++c) h[c] = (int32_t)x[c];
+        a.ancestry[(size_t)chain * a.anc_stride + j] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.log_zeta[(size_t)chain * a.T] = 0.0;
+    if (a.T > 1) {
+        double w = 0.0;
+        if (j < a.N) w = particle_weight<MODEL, G, OBS>(x, a.Y, cp, a.lf, a.lf_max);
+        const size_t wbase = (size_t)chain * a.wstride;            // buffer 0
+        const double loc = block_inclusive_scan<WG>(w, smem);
+        a.wraw[wbase + j] = w;
+        a.wloc[wbase + j] = loc;
+        if (threadIdx.x == WG - 1) a.bsum[(size_t)chain * a.bstride + blockIdx.x] = loc;
+    }
+}
+
+template <int MODEL, int G, int OBS, int WG>
+__global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
+    using Sh = Shape<MODEL, G>;
+    constexpr int C = Sh::C;
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* red = smem;                  // WG/64 (+pad)
+    double* bsum = smem + 16;            // B
+    double* bpex = bsum + a.B;           // B + WG
+    const int chain = blockIdx.y;
+    const int tid = threadIdx.x;
+    const int j = blockIdx.x * WG + tid;
+    if (a.status[chain] != 0) return;
+    const ChainParam cp = a.cp[chain];
+    const int prev = (p - 1) & 1, cur = p & 1;
+    const size_t wprev = ((size_t)prev * a.max_chains + chain) * a.wstride;
+    const size_t wcur = ((size_t)cur * a.max_chains + chain) * a.wstride;
+    const size_t bprev = ((size_t)prev * a.max_chains + chain) * a.bstride;
+    const size_t bcur = ((size_t)cur * a.max_chains + chain) * a.bstride;
+
+    // (b) likelihood: zetas[p] = zetas[p-1] * mean(w)  (pmcmc.py:183), kept in log space
+    const double total = scan_block_sums<WG>(a.bsum + bprev, a.B, bpex, bsum, red);
+    if (!(total > 0.0)) {  // all weights 0 or NaN: numpy raises ValueError -> (None, None, None), :187-192
+        if (blockIdx.x == 0 && tid == 0) {
+            a.status[chain] = 1;
+            a.log_zeta[(size_t)chain * a.T + p] = -__builtin_inf();
+        }
+        return;
+    }
+    if (blockIdx.x == 0 && tid == 0)
+        a.log_zeta[(size_t)chain * a.T + p] = a.log_zeta[(size_t)chain * a.T + p - 1] + log(total / (double)a.N);
+
+    int nev = 0;
+    double w = 0.0;
+    if (j < a.N) {
+        // (d) multinomial (or systematic) draw and certified search, pmcmc.py:188-190
+        double U;
+        const uint32_t rtag = ((uint32_t)p & 0xFFFFFFu) | kDomainResample;
+        if (a.resample_mode == 0) {
+            const Block r = philox(0u, (uint32_t)j, rtag, cp.f, cp.k0, cp.k1);
+            U = u01(r.x, r.y);
+        } else {
+            const Block r = philox(0u, 0u, rtag, cp.f, cp.k0, cp.k1);
+            U = ((double)j + u01(r.x, r.y)) / (double)a.N;
+        }
+        bool fb;
+        int anc = resample_search<WG>(U, bpex, bsum, a.B, total, a.wloc + wprev, a.wraw + wprev, a.N, a.delta, fb);
+        anc = min(max(anc, 0), a.N - 1);
+        if (fb) atomicAdd(a.counters + 1, 1ull);
+        a.ancestry[(size_t)chain * a.anc_stride + (size_t)p * a.N + j] = anc;   // :193
+        // (f) gather the parent state, (g) propagate over [0, 1], :195-220
+        const int32_t* hp = a.hidden + (size_t)chain * a.hist_stride + ((size_t)(p - 1) * a.N + anc) * C;
+        double x[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) x[c] = (double)hp[c];
+        const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
+        nev = ssa_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0);
+        int32_t* hc = a.hidden + (size_t)chain * a.hist_stride + ((size_t)p * a.N + j) * C;
+#pragma unroll
+        for (int c = 0; c < C; ++c) hc[c] = (int32_t)x[c];                        // :222-231
+        // (a) weights of the new state against Y[p], used by step p+1, :178-181
+        if (p + 1 < a.T) w = particle_weight<MODEL, G, OBS>(x, a.Y + (size_t)p * Sh::K, cp, a.lf, a.lf_max);
+    }
+    if (a.count_events) {
+        unsigned long long e = (unsigned long long)nev;
+        for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
+        if ((tid & 63) == 0) atomicAdd(a.counters, e);
+    }
+    if (p + 1 < a.T) {
+        const double loc = block_inclusive_scan<WG>(w, red);
+        a.wraw[wcur + j] = w;
+        a.wloc[wcur + j] = loc;
+        if (tid == WG - 1) a.bsum[bcur + blockIdx.x] = loc;
+    }
+}
+
+// particle_path_sampler, pmcmc.py:236-248 (one lane per chain; T dependent loads)
+__global__ void path_sample_kernel(PathArgs a) {
+    const int chain = blockIdx.x * blockDim.x + threadIdx.x;
+    if (chain >= a.n_chains) return;
+    int chosen = min(max(a.chosen[chain], 0), a.N - 1);
+    const int32_t* hid = a.hidden + (size_t)chain * a.hist_stride;
+    const int32_t* anc = a.ancestry + (size_t)chain * a.anc_stride;
+    int32_t* out = a.traj + (size_t)chain * a.T * a.C;
+    for (int c = 0; c < a.C; ++c) out[(size_t)(a.T - 1) * a.C + c] = hid[((size_t)(a.T - 1) * a.N + chosen) * a.C + c];
+    for (int p = a.T - 2; p >= 0; --p) {
+        chosen = min(max(anc[(size_t)p * a.N + chosen], 0), a.N - 1);     // ancestry[p], as the reference
+        for (int c = 0; c < a.C; ++c) out[(size_t)p * a.C + c] = hid[((size_t)p * a.N + chosen) * a.C + c];
+    }
+}
+
+template <int MODEL, int G>
+__global__ __launch_bounds__(256) void simulate_kernel(SimArgs a) {
+    constexpr int C = Shape<MODEL, G>::C;
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    int nev = 0;
+    if (j < a.n) {
+        double x[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) x[c] = (double)a.in[(size_t)j * C + c];
+        nev = ssa_propagate<MODEL, G>(x, *a.cp, (uint32_t)j, (a.step & 0xFFFFFFu) | kDomainSSA, a.tmax);
+#pragma unroll
+        for (int c = 0; c < C; ++c) a.out[(size_t)j * C + c] = (int32_t)x[c];
+    }
+    unsigned long long e = (unsigned long long)nev;
+    for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(a.events, e);
+}
+
+// Standalone resampler over caller-supplied weights and uniforms (same scan + search code as the filter).
+template <int WG>
+__global__ __launch_bounds__(WG) void resample_scan_kernel(ResampleArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int j = blockIdx.x * WG + threadIdx.x;
+    const double w = (j < a.N) ? a.w[j] : 0.0;
+    const double loc = block_inclusive_scan<WG>(w, smem);
+    a.wraw[j] = w;
+    a.wloc[j] = loc;
+    if (threadIdx.x == WG - 1) a.bsum[blockIdx.x] = loc;
+}
+
+template <int WG>
+__global__ __launch_bounds__(WG) void resample_search_kernel(ResampleArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    double* red = smem;
+    double* bsum = smem + 16;
+    double* bpex = bsum + a.B;
+    const int j = blockIdx.x * WG + threadIdx.x;
+    const double total = scan_block_sums<WG>(a.bsum, a.B, bpex, bsum, red);
+    if (!(total > 0.0)) {
+        if (j == 0) *a.status = 1;
+        return;
+    }
+    if (j < a.N) {
+        bool fb;
+        const int anc = resample_search<WG>(a.u[j], bpex, bsum, a.B, total, a.wloc, a.wraw, a.N, a.delta, fb);
+        a.out[j] = min(max(anc, 0), a.N - 1);
+        if (fb) atomicAdd(a.fallbacks, 1ull);
+    }
+}
+
+// ------------------------------------------------------------------------------- launchers
+size_t step_lds_bytes(int B, int wg) { return sizeof(double) * (size_t)(16 + B + B + wg); }
+
+template <int MODEL, int G, int OBS, int WG>
+static hipError_t launch_filter_t(const StepArgs& a, int n_chains, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
+                                  hipEvent_t ev2) {
+    const dim3 grid(a.B, n_chains), block(WG);
+    const size_t lds = step_lds_bytes(a.B, WG);
+    if (ev0) (void)hipEventRecord(ev0, s);
+    hipLaunchKernelGGL((pf_init_kernel<MODEL, G, OBS, WG>), grid, block, lds, s, a);
+    if (ev1) (void)hipEventRecord(ev1, s);
+    for (int p = 1; p < a.T; ++p)
+        hipLaunchKernelGGL((pf_step_kernel<MODEL, G, OBS, WG>), grid, block, lds, s, a, p);
+    if (ev2) (void)hipEventRecord(ev2, s);
+    return hipGetLastError();
+}
+
+template <int MODEL, int G, int WG>
+static hipError_t launch_obs(const StepArgs& a, int obs, int n_chains, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
+                             hipEvent_t e2) {
+    return obs == kBinomial ? launch_filter_t<MODEL, G, kBinomial, WG>(a, n_chains, s, e0, e1, e2)
+                            : launch_filter_t<MODEL, G, kNormal, WG>(a, n_chains, s, e0, e1, e2);
+}
+
+template <int WG>
+static hipError_t launch_model(const StepArgs& a, int model, int G, int obs, int n_chains, hipStream_t s,
+                               hipEvent_t e0, hipEvent_t e1, hipEvent_t e2) {
+    switch (model) {
+        case kSIR: return launch_obs<kSIR, 1, WG>(a, obs, n_chains, s, e0, e1, e2);
+        case kSEIR: return launch_obs<kSEIR, 1, WG>(a, obs, n_chains, s, e0, e1, e2);
+        case kSubgroups:
+            switch (G) {
+                case 1: return launch_obs<kSubgroups, 1, WG>(a, obs, n_chains, s, e0, e1, e2);
+                case 2: return launch_obs<kSubgroups, 2, WG>(a, obs, n_chains, s, e0, e1, e2);
+                case 3: return launch_obs<kSubgroups, 3, WG>(a, obs, n_chains, s, e0, e1, e2);
+                case 4: return launch_obs<kSubgroups, 4, WG>(a, obs, n_chains, s, e0, e1, e2);
+            }
+            break;
+        case kSubgroups2:
+            switch (G) {
+                case 1: return launch_obs<kSubgroups2, 1, WG>(a, obs, n_chains, s, e0, e1, e2);
+                case 2: return launch_obs<kSubgroups2, 2, WG>(a, obs, n_chains, s, e0, e1, e2);
+                case 3: return launch_obs<kSubgroups2, 3, WG>(a, obs, n_chains, s, e0, e1, e2);
+                case 4: return launch_obs<kSubgroups2, 4, WG>(a, obs, n_chains, s, e0, e1, e2);
+            }
+            break;
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, hipStream_t s,
+                         hipEvent_t ev_init, hipEvent_t ev_step0, hipEvent_t ev_end) {
+    if (a.wg == 64) return launch_model<64>(a, model, G, obs, n_chains, s, ev_init, ev_step0, ev_end);
+    return launch_model<256>(a, model, G, obs, n_chains, s, ev_init, ev_step0, ev_end);
+}
+
+hipError_t launch_path_sample(const PathArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(path_sample_kernel, dim3((a.n_chains + 63) / 64), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+template <int MODEL, int G>
+static void sim_t(const SimArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL((simulate_kernel<MODEL, G>), dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+}
+
+hipError_t launch_simulate(const SimArgs& a, int model, int G, hipStream_t s) {
+    switch (model) {
+        case kSIR: sim_t<kSIR, 1>(a, s); break;
+        case kSEIR: sim_t<kSEIR, 1>(a, s); break;
+        default:
+            switch (G) {
+                case 1: sim_t<kSubgroups, 1>(a, s); break;
+                case 2: sim_t<kSubgroups, 2>(a, s); break;
+                case 3: sim_t<kSubgroups, 3>(a, s); break;
+                case 4: sim_t<kSubgroups, 4>(a, s); break;
+                default: return hipErrorInvalidValue;
+            }
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_resample(const ResampleArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(resample_scan_kernel<256>, dim3(a.B), dim3(256), sizeof(double) * 16, s, a);
+    hipLaunchKernelGGL(resample_search_kernel<256>, dim3(a.B), dim3(256), step_lds_bytes(a.B, 256), s, a);
+    return hipGetLastError();
+}
+
+}  // namespace epipf

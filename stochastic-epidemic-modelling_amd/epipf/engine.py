@@ -1,0 +1,180 @@
+"""Engine: one libepipf context (device buffers for a model / particle-count / horizon / chain batch).
+
+This is the layer the drop-in `particle_filter` / `particle_mcmc` call.  An engine keeps the
+observations, the log-factorial table and the whole particle history resident in HBM; a batched
+`run()` moves only per-chain parameters in and log-likelihoods + status out.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ptr
+
+MODEL_IDS = {"sir": _lib.SIR, "seir": _lib.SEIR, "sir_subgroups": _lib.SIR_SUBGROUPS,
+             "sir_subgroups2": _lib.SIR_SUBGROUPS2}
+
+
+def model_id(type_model):
+    """Accept this package's ModelType, the reference's ModelType (same .value strings) or a string."""
+    name = getattr(type_model, "value", type_model)
+    if isinstance(name, str) and name.lower() in MODEL_IDS:
+        return MODEL_IDS[name.lower()]
+    raise ValueError(f"unknown model type {type_model!r}")
+
+
+def n_compartments(mid, G):
+    return 3 if mid == _lib.SIR else 4 if mid == _lib.SEIR else 3 * G
+
+
+def theta_vector(mid, theta):
+    """Flatten a reference theta: SIR/SEIR arrays, or (beta[G][G], gamma) for the subgroup models
+    (pmcmc.py:211-218 passes theta_proposal[0], theta_proposal[1])."""
+    if mid in (_lib.SIR_SUBGROUPS, _lib.SIR_SUBGROUPS2):
+        beta, gamma = theta
+        beta = np.asarray(beta, dtype=np.float64)
+        if beta.ndim != 2 or beta.shape[0] != beta.shape[1]:
+            raise ValueError("subgroup theta must be (beta[G][G], gamma)")
+        return np.append(beta.reshape(-1), float(gamma)), beta.shape[0]
+    th = np.asarray(theta, dtype=np.float64).reshape(-1)
+    need = 2 if mid == _lib.SIR else 3
+    if th.size != need:
+        raise ValueError(f"theta must have {need} entries for this model, got {th.size}")
+    return th, 1
+
+
+class Engine:
+    def __init__(self, type_model, groups=1, n_particles=1000, t_max=1, max_chains=1, device=0):
+        L = _lib.load()
+        self.model = model_id(type_model)
+        self.G = int(groups) if self.model >= _lib.SIR_SUBGROUPS else 1
+        self.C = n_compartments(self.model, self.G)
+        self.K = 3 if self.model == _lib.SIR_SUBGROUPS2 else self.C
+        self.N = int(n_particles)
+        self.t_max = int(t_max)
+        self.max_chains = int(max_chains)
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        check(L.epipf_create(ctypes.byref(h), self.device, self.model, self.G, self.N, self.t_max, self.max_chains),
+              "epipf_create")
+        self._h = h
+        self._L = L
+        self._Y = None
+        self._pop = None
+        self.T = 0
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.epipf_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ inputs
+    def set_observations(self, Y):
+        Y = np.ascontiguousarray(np.asarray(Y, dtype=np.float64))
+        if Y.ndim != 2:
+            raise ValueError("Y must be 2-D [T, K]")
+        if self._Y is not None and self._Y.shape == Y.shape and np.array_equal(self._Y, Y, equal_nan=True):
+            return
+        check(self._L.epipf_set_observations(self._h, ptr(Y), Y.shape[0], Y.shape[1]), "epipf_set_observations")
+        self._Y = Y.copy()
+        self.T = Y.shape[0]
+
+    def set_population(self, n_population, mu):
+        npop = np.ascontiguousarray(np.atleast_1d(np.asarray(n_population, dtype=np.float64)))
+        mus = np.ascontiguousarray(np.atleast_1d(np.asarray(mu, dtype=np.float64)))
+        if npop.size != self.G or mus.size != self.G:
+            raise ValueError(f"n_population and mu need {self.G} entries")
+        key = (tuple(npop), tuple(mus))
+        if key == self._pop:
+            return
+        check(self._L.epipf_set_population(self._h, ptr(npop), ptr(mus)), "epipf_set_population")
+        self._pop = key
+
+    # ------------------------------------------------------------------ the filter
+    def run(self, thetas, probs, keys, filter_indices, observations=False, active=None, resample="multinomial"):
+        """Run len(thetas) independent filters.  Returns (log_zetas [n, T], status [n])."""
+        thetas = np.ascontiguousarray(np.asarray(thetas, dtype=np.float64))
+        n = thetas.shape[0]
+        probs = np.ascontiguousarray(np.broadcast_to(np.asarray(probs, dtype=np.float64), (n,)))
+        keys = np.ascontiguousarray(np.broadcast_to(np.asarray(keys, dtype=np.uint64), (n,)))
+        fidx = np.ascontiguousarray(np.broadcast_to(np.asarray(filter_indices, dtype=np.uint64), (n,))
+                                    .astype(np.uint32))
+        act = None if active is None else np.ascontiguousarray(np.asarray(active, dtype=np.int32))
+        lz = np.empty((n, self.T), dtype=np.float64)
+        st = np.empty(n, dtype=np.int32)
+        mode = _lib.RESAMPLE_MULTINOMIAL if resample == "multinomial" else _lib.RESAMPLE_SYSTEMATIC
+        check(self._L.epipf_run(self._h, n, ptr(thetas), thetas.shape[1],
+                                _lib.OBS_NORMAL if observations else _lib.OBS_BINOMIAL, ptr(probs), ptr(keys),
+                                ptr(fidx), ptr(act), mode, ptr(lz), ptr(st)), "epipf_run")
+        self._last_n = n
+        return lz, st
+
+    def history(self, n_chains=None):
+        """(hidden [n, T, N, C] int32, ancestry [n, T, N] int32) of the last run."""
+        n = self._last_n if n_chains is None else int(n_chains)
+        hid = np.empty((n, self.T, self.N, self.C), dtype=np.int32)
+        anc = np.empty((n, self.T, self.N), dtype=np.int32)
+        check(self._L.epipf_copy_history(self._h, n, ptr(hid), ptr(anc)), "epipf_copy_history")
+        return hid, anc
+
+    def path_sample(self, chosen):
+        chosen = np.ascontiguousarray(np.asarray(chosen, dtype=np.int32).reshape(-1))
+        out = np.empty((chosen.size, self.T, self.C), dtype=np.int32)
+        check(self._L.epipf_path_sample(self._h, chosen.size, ptr(chosen), ptr(out)), "epipf_path_sample")
+        return out
+
+    # ------------------------------------------------------------------ aux entry points
+    def simulate(self, states, theta, max_time=1.0, key=0, filter_index=0, step=0):
+        states = np.ascontiguousarray(np.asarray(states, dtype=np.int32).reshape(-1, self.C))
+        th, _ = theta_vector(self.model, theta)
+        th = np.ascontiguousarray(th)
+        out = np.empty_like(states)
+        ev = np.zeros(1, dtype=np.int64)
+        check(self._L.epipf_simulate(self._h, states.shape[0], ptr(states), ptr(th), th.size, float(max_time),
+                                     int(key) & (2**64 - 1), int(filter_index) & 0xFFFFFFFF, int(step), ptr(out),
+                                     ptr(ev)), "epipf_simulate")
+        return out, int(ev[0])
+
+    def resample(self, w, u):
+        w = np.ascontiguousarray(np.asarray(w, dtype=np.float64))
+        u = np.ascontiguousarray(np.asarray(u, dtype=np.float64))
+        out = np.empty(w.size, dtype=np.int32)
+        fb = np.zeros(1, dtype=np.int64)
+        rc = check(self._L.epipf_resample(self._h, w.size, ptr(w), ptr(u), ptr(out), ptr(fb)), "epipf_resample")
+        return (None if rc == _lib.STATUS_DEGENERATE else out), int(fb[0])
+
+    # ------------------------------------------------------------------ stats
+    def set_profiling(self, on=True):
+        check(self._L.epipf_set_profiling(self._h, 1 if on else 0), "epipf_set_profiling")
+
+    def stats(self):
+        s = _lib.Stats()
+        check(self._L.epipf_get_stats(self._h, ctypes.byref(s)), "epipf_get_stats")
+        return s.as_dict()
+
+    def reset_stats(self):
+        check(self._L.epipf_reset_stats(self._h), "epipf_reset_stats")
+
+
+_CACHE = {}
+
+
+def get_engine(type_model, groups, n_particles, T, chains=1, device=0):
+    """Cached engine large enough for (T, chains); grows by re-creating when a bigger one is needed."""
+    mid = model_id(type_model)
+    key = (mid, groups if mid >= _lib.SIR_SUBGROUPS else 1, int(n_particles), int(device))
+    eng = _CACHE.get(key)
+    if eng is None or eng.t_max < T or eng.max_chains < chains:
+        if eng is not None:
+            eng.close()
+        eng = Engine(type_model, groups, n_particles, max(T, eng.t_max if eng else 0),
+                     max(chains, eng.max_chains if eng else 0), device)
+        _CACHE[key] = eng
+    return eng

@@ -1,0 +1,375 @@
+"""Drop-in particle filter / PMCMC with the reference's call surface, running on MI355X.
+
+Mirrors /root/reference/pmcmc.py:
+  ModelType               pmcmc.py:116-120
+  particle_filter         pmcmc.py:123-233   -> libepipf epipf_run (one GPU lane per particle)
+  particle_path_sampler   pmcmc.py:236-248   (host version for arrays; particle_mcmc uses the device one)
+  particle_mcmc           pmcmc.py:251-408   (host MH loop; filter + path sampling on the GPU)
+plus `particle_mcmc_chains`, the same sampler run for several independent chains in lockstep, each
+chain one GPU-batched filter per MH iteration.
+
+Random numbers.  The reference draws everything from numpy's global MT19937.  Here:
+  * MH proposals (multivariate_normal), acceptance uniforms and the path sampler's randint stay on
+    the host RandomState (the global one by default), called in the reference's order;
+  * the filter's own draws (initial Poisson states, resampling, Gillespie events) come from the keyed
+    Philox stream: key = `key` (default: the module stream, see `seed_stream`), filter
+    index = one per particle-filter call.
+Under np.random.seed(s) + seed_stream(k) the results equal the reference's driven by the same
+keyed stream (tests/golden/make_golden.py), which is how parity is tested.
+"""
+import math
+from enum import Enum
+
+import numpy as np
+
+from . import _lib
+from .engine import get_engine, model_id, n_compartments, theta_vector
+
+
+class ModelType(Enum):
+    SIR = "sir"
+    SEIR = "seir"
+    SIR_SUBGROUPS = "sir_subgroups"
+    SIR_SUBGROUPS2 = "sir_subgroups2"
+
+
+class _Stream:
+    key = 0
+    next_filter = 0
+
+
+_STREAM = _Stream()
+
+
+def seed_stream(key, filter_index=0):
+    """Set the module's Philox key and reset its filter counter (the analogue of np.random.seed for
+    the filter's own draws)."""
+    _STREAM.key = int(key) & (2**64 - 1)
+    _STREAM.next_filter = int(filter_index)
+
+
+def _take_filter_index():
+    f = _STREAM.next_filter
+    _STREAM.next_filter += 1
+    return f
+
+
+def chain_key(key, chain):
+    """Philox key of chain `chain` of a multi-chain run (chain 0 keeps `key`)."""
+    return (int(key) + (int(chain) << 32)) & (2**64 - 1)
+
+
+def _population(mid, G, n_population, mu):
+    if mid >= _lib.SIR_SUBGROUPS:
+        npop = np.atleast_1d(np.asarray(n_population, dtype=np.float64))
+        mus = np.atleast_1d(np.asarray(mu, dtype=np.float64))
+        if npop.size != G or mus.size != G:
+            raise ValueError("subgroup models need n_population and mu with one entry per group")
+        return npop, mus
+    return np.array([float(n_population)]), np.array([float(mu)])
+
+
+def _check_Y(mid, G, Y):
+    Y = np.asarray(Y, dtype=np.float64)
+    if Y.ndim != 2:
+        raise ValueError("Y must be a 2-D array [T, K]")
+    K = 3 if mid == _lib.SIR_SUBGROUPS2 else n_compartments(mid, G)
+    if Y.shape[1] != K:
+        raise ValueError(f"Y has {Y.shape[1]} columns, model observes {K}")
+    return Y
+
+
+def particle_filter(Y, type_model, theta_proposal, observations=False, probs=.1, n_particles=1000,
+                    n_population=4820, mu=20, jobs=4, *, key=None, filter_index=None, resample="multinomial",
+                    device=0, return_history=True):
+    """pmcmc.py:123-233.  Returns (zetas[T], hidden_process[T,N,C], ancestry_matrix[T,N]) as float64,
+    or (None, None, None) when every weight of some step is 0/NaN (the reference's ValueError path).
+    `jobs` is accepted for compatibility and ignored (one GPU lane per particle)."""
+    mid = model_id(type_model)
+    th, G = theta_vector(mid, theta_proposal)
+    Y = _check_Y(mid, G, Y)
+    npop, mus = _population(mid, G, n_population, mu)
+    eng = get_engine(mid, G, n_particles, Y.shape[0], 1, device)
+    eng.set_observations(Y)
+    eng.set_population(npop, mus)
+    k = _STREAM.key if key is None else key
+    f = _take_filter_index() if filter_index is None else filter_index
+    lz, st = eng.run(th[None, :], [probs], [k], [f], observations=observations, resample=resample)
+    if st[0] != _lib.STATUS_OK:
+        return None, None, None
+    zetas = np.exp(lz[0])
+    if not return_history:
+        return zetas, None, None
+    hid, anc = eng.history(1)
+    return zetas, hid[0].astype(np.float64), anc[0].astype(np.float64)
+
+
+def particle_path_sampler(hidden_process, ancestry_matrix):
+    """pmcmc.py:236-248, unchanged semantics (uniform final pick; ancestry[p] indexing)."""
+    n_particles = hidden_process.shape[1]
+    time_steps = hidden_process.shape[0]
+    trajectory = np.zeros((time_steps, hidden_process.shape[2]))
+    chosen_path = np.random.randint(0, n_particles)
+    trajectory[-1, :] = hidden_process[-1, chosen_path, :]
+    for p in range(time_steps - 2, -1, -1):
+        chosen_path = int(ancestry_matrix[p, chosen_path])
+        trajectory[p, :] = hidden_process[p, chosen_path, :]
+    return trajectory
+
+
+# ---------------------------------------------------------------------------------------- MH
+def _reference_ratio(z_new, z_old, theta_new, theta_old, parameters, cov):
+    """The reference's acceptance probability, pmcmc.py:376-393, evaluated verbatim (np.float64)."""
+    from scipy.stats import multivariate_normal
+    if "e" in str(z_new):
+        constant = int(str(z_new).split("e-")[-1]) // 2
+    else:
+        constant = 1
+    prob = (
+        1e1 ** constant
+        * multivariate_normal.pdf(theta_new, np.array(parameters), cov)
+        * multivariate_normal.pdf(theta_old, theta_new, cov)
+        * z_new
+    )
+    prob /= (
+        1e1 ** constant
+        * multivariate_normal.pdf(np.array(parameters), theta_new, cov)
+        * multivariate_normal.pdf(theta_new, theta_old, cov)
+        * z_old
+    )
+    return min(1, prob)
+
+
+def _log_ratio(lz_new, lz_old):
+    """Underflow-free MH acceptance probability min(1, z'/z) from log-likelihoods (the symmetric
+    Gaussian proposal terms of pmcmc.py:380-391 cancel)."""
+    lr = lz_new - lz_old
+    if math.isnan(lr):
+        return 0.0
+    return min(1.0, math.exp(min(lr, 0.0)))
+
+
+class ChainResult:
+    """Per-chain outputs in the reference's layout plus run counters."""
+
+    def __init__(self, thetas, likelihoods, log_likelihoods, sampled_trajs, acceptances, filters_run):
+        self.thetas = thetas
+        self.likelihoods = likelihoods
+        self.log_likelihoods = log_likelihoods
+        self.sampled_trajs = sampled_trajs
+        self.acceptances = acceptances
+        self.filters_run = filters_run
+
+
+class ChainSampler:
+    """Lockstep random-walk PMCMC over `chains` independent chains (pmcmc.py:251-408 each), one batched
+    GPU filter per MH iteration.  `iters` keeps the reference's `n_chains` meaning (MH iterations per
+    chain).  Use `initialise()` then `step()` iters-1 times (or `run()`); results via `results()`.
+
+    rngs: per-chain RandomState-like objects (proposals, path picks, acceptance uniforms).
+    keys: per-chain Philox keys for the filters; filter indices count from `filter_index_start`."""
+
+    def __init__(self, Y, type_model, parameters, h, adaptive=False, sigma=None, iters=1000, observations=False,
+                 probs=.1, n_particles=1000, n_population=4820, mu=20, *, rngs, keys, device=0,
+                 mh_ratio="reference", resample="multinomial", filter_index_start=0):
+        self.rngs = list(rngs)
+        self.keys = np.asarray(keys, dtype=np.uint64)
+        nc = self.nc = len(self.rngs)
+        mid = self.mid = model_id(type_model)
+        d = self.d = len(parameters)
+        self.parameters = list(parameters)
+        self.probs = probs
+        self.h = h
+        self.adaptive = adaptive
+        self.observations = observations
+        self.mh_ratio = mh_ratio
+        self.resample = resample
+        self.N = int(n_particles)
+        G = int(round(math.sqrt(d - (2 if probs is None else 1)))) if mid >= _lib.SIR_SUBGROUPS else 1
+        Y = _check_Y(mid, G, Y)
+        T = self.T = Y.shape[0]
+        Cc = n_compartments(mid, G)
+        npop, mus = _population(mid, G, n_population, mu)
+        self.iters = int(iters)
+        eng = self.eng = get_engine(mid, G, n_particles, T, nc, device)
+        eng.set_observations(Y)
+        eng.set_population(npop, mus)
+        self.thetas = np.zeros((nc, self.iters, d))
+        self.likelihoods = np.zeros((nc, self.iters))
+        self.loglik = np.zeros((nc, self.iters))
+        self.trajs = np.zeros((nc, T, self.iters, Cc))
+        self.std = [np.eye(d) if sigma is None else np.asarray(sigma, dtype=np.float64) for _ in range(nc)]
+        self.fnext = [int(filter_index_start)] * nc
+        self.filters_run = [0] * nc
+        self.acceptances = [1] * nc
+        self.dth = d - (1 if probs is None else 0)
+        self.i = 0
+        self.last_active = 0
+
+    def _split(self, prop):
+        """probs / subgroup reshaping, pmcmc.py:283-296 and :339-352 (the subgroup beta matrix is the
+        row-major flattening of theta[:G*G], i.e. theta itself)."""
+        if self.probs is None:
+            probs2 = min(prop[-1], 1)
+            probs2 = max(probs2, 0)
+            return prop[:-1], probs2
+        return prop, self.probs
+
+    def _run_batch(self, props):
+        nc = self.nc
+        th_all = np.zeros((nc, self.dth))
+        pr_all = np.zeros(nc)
+        act = np.zeros(nc, dtype=np.int32)
+        fidx = np.zeros(nc, dtype=np.uint64)
+        stripped = {}
+        for c, prop in props.items():
+            th, p2 = self._split(prop)
+            stripped[c] = (th, p2)
+            th_all[c] = th
+            pr_all[c] = p2
+            act[c] = 1
+            fidx[c] = self.fnext[c]
+            self.fnext[c] += 1
+            self.filters_run[c] += 1
+        lz, st = self.eng.run(th_all, pr_all, self.keys, fidx, observations=self.observations, active=act,
+                              resample=self.resample)
+        self.last_active = len(props)
+        return lz, st, stripped
+
+    def _path_sample(self, ok):
+        chosen = np.zeros(self.nc, dtype=np.int32)
+        for c in ok:
+            chosen[c] = self.rngs[c].randint(0, self.N)            # pmcmc.py:241, host RNG order kept
+        return self.eng.path_sample(chosen)
+
+    def _copy_prev(self, c, i):
+        self.thetas[c, i] = self.thetas[c, i - 1]
+        self.likelihoods[c, i] = self.likelihoods[c, i - 1]
+        self.loglik[c, i] = self.loglik[c, i - 1]
+        self.trajs[c, :, i, :] = self.trajs[c, :, i - 1, :]
+
+    def initialise(self):
+        """The initial draw loop, pmcmc.py:276-318 (repeat until theta >= 0 and the filter succeeded)."""
+        pending = list(range(self.nc))
+        while pending:
+            props = {}
+            for c in pending:
+                prop = self.rngs[c].multivariate_normal(np.array(self.parameters), self.h * self.std[c])
+                if sum(prop < 0) > 0:
+                    continue
+                props[c] = prop
+            if not props:
+                continue
+            lz, st, stripped = self._run_batch(props)
+            ok = [c for c in props if st[c] == _lib.STATUS_OK]
+            if ok:
+                tr = self._path_sample(ok)
+                for c in ok:
+                    th, p2 = stripped[c]
+                    if self.probs is None:
+                        th = np.append(th, p2)
+                    self.thetas[c, 0] = th
+                    self.loglik[c, 0] = lz[c, -1]
+                    self.likelihoods[c, 0] = np.exp(lz[c, -1])
+                    self.trajs[c, :, 0, :] = tr[c]
+            pending = [c for c in pending if c not in ok]
+        self.i = 1
+
+    def step(self):
+        """One MH iteration for every chain, pmcmc.py:325-406.  Returns the number of chains that ran a filter."""
+        i = self.i
+        props = {}
+        for c in range(self.nc):
+            if self.adaptive and i > 1e3:
+                self.std[c] = np.cov(self.thetas[c, :i].T, ddof=0) + 1e-4 * np.eye(self.d)
+            prop = self.rngs[c].multivariate_normal(self.thetas[c, i - 1], self.h * self.std[c])
+            if sum(prop < 0) > 0:
+                self._copy_prev(c, i)
+                continue
+            props[c] = prop
+        if props:
+            lz, st, stripped = self._run_batch(props)
+            ok = [c for c in props if st[c] == _lib.STATUS_OK]
+            tr = self._path_sample(ok) if ok else None
+            for c in props:
+                if st[c] != _lib.STATUS_OK:
+                    self._copy_prev(c, i)
+                    continue
+                th, p2 = stripped[c]
+                theta_new = np.append(th, p2) if self.probs is None else props[c]
+                z_new = np.exp(lz[c, -1])
+                if self.mh_ratio == "reference":
+                    prob = _reference_ratio(z_new, self.likelihoods[c, i - 1], theta_new, self.thetas[c, i - 1],
+                                            self.parameters, self.h * self.std[c])
+                else:
+                    prob = _log_ratio(lz[c, -1], self.loglik[c, i - 1])
+                if self.rngs[c].uniform() < prob:
+                    self.acceptances[c] += 1
+                    self.thetas[c, i] = theta_new
+                    self.likelihoods[c, i] = z_new
+                    self.loglik[c, i] = lz[c, -1]
+                    self.trajs[c, :, i, :] = tr[c]
+                else:
+                    self._copy_prev(c, i)
+        self.i += 1
+        return len(props)
+
+    def run(self, progress=False, on_iteration=None):
+        if self.i == 0:
+            self.initialise()
+        bar = None
+        if progress:
+            from tqdm import tqdm
+            bar = tqdm(total=self.iters - 1, desc="Chains", position=1)
+        while self.i < self.iters:
+            n = self.step()
+            if bar is not None:
+                i = self.i - 1
+                bar.update(1)
+                bar.set_postfix_str(f"accepted_theta: {self.thetas[0, i]}, "
+                                    f"acceptance_ratio: {100 * self.acceptances[0] / (i + 1)}%")
+            if on_iteration is not None:
+                on_iteration(self.i - 1, n)
+        if bar is not None:
+            bar.close()
+        return self.results()
+
+    def results(self):
+        return [ChainResult(self.thetas[c], self.likelihoods[c], self.loglik[c], self.trajs[c], self.acceptances[c],
+                            self.filters_run[c]) for c in range(self.nc)]
+
+
+def particle_mcmc_chains(Y, type_model, parameters, h, adaptive=False, sigma=None, n_chains=1000,
+                         observations=False, probs=.1, n_particles=1000, n_population=4820, mu=20, *,
+                         rngs=None, keys=None, chains=1, seed=0, device=0, mh_ratio="reference",
+                         resample="multinomial", progress=False, filter_index_start=0, on_iteration=None):
+    """Run `chains` independent PMCMC chains (pmcmc.py:251-408 each) in lockstep.  `n_chains` keeps the
+    reference's meaning: MH iterations per chain.  Default rngs: np.random.RandomState(seed + c); default
+    keys: chain_key(seed, c).  Returns a list of ChainResult."""
+    if rngs is None:
+        rngs = [np.random.RandomState(seed + c) for c in range(chains)]
+    if keys is None:
+        keys = [chain_key(seed, c) for c in range(len(rngs))]
+    sampler = ChainSampler(Y, type_model, parameters, h, adaptive, sigma, n_chains, observations, probs, n_particles,
+                           n_population, mu, rngs=rngs, keys=keys, device=device, mh_ratio=mh_ratio,
+                           resample=resample, filter_index_start=filter_index_start)
+    return sampler.run(progress=progress, on_iteration=on_iteration)
+
+
+def particle_mcmc(Y, type_model, parameters, h, adaptive=False, sigma=None, n_chains=1000, observations=False,
+                  probs=.1, n_particles=1000, n_population=4820, mu=20, jobs=4, *, key=None, device=0,
+                  mh_ratio="reference", resample="multinomial", progress=True):
+    """pmcmc.py:251-408 with the same signature and return value (thetas, likelihoods, sampled_trajs).
+
+    Uses numpy's GLOBAL RandomState for proposals / acceptance / path picks, as the reference, and the
+    module Philox stream (seed_stream) for the filters.  mh_ratio="reference" evaluates the reference's
+    acceptance expression verbatim (linear likelihoods, MVN factors); "log" uses log-likelihoods and
+    stays correct when the likelihood underflows (T ≳ 150 observations)."""
+    k = _STREAM.key if key is None else key
+    res = particle_mcmc_chains(Y, type_model, parameters, h, adaptive, sigma, n_chains, observations, probs,
+                               n_particles, n_population, mu, rngs=[np.random], keys=[k], device=device,
+                               mh_ratio=mh_ratio, resample=resample, progress=progress,
+                               filter_index_start=_STREAM.next_filter)[0]
+    if key is None:
+        _STREAM.next_filter += res.filters_run
+    return res.thetas, res.likelihoods, res.sampled_trajs.astype(np.float64)

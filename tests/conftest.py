@@ -1,0 +1,66 @@
+"""Shared test setup.  `-m "not gpu"` runs on CPU; `-m gpu` needs an MI355X and libepipf.so."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "stochastic-epidemic-modelling_amd")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+for p in (REPO, PKG, os.path.join(REPO, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD GPU (MI355X) and the built libepipf.so")
+
+
+_CACHE = {}
+
+
+def load_golden(fname):
+    """{case: {field: array}} from a tests/golden/*.npz written by make_golden.py."""
+    if fname not in _CACHE:
+        z = np.load(os.path.join(GOLDEN, fname), allow_pickle=False)
+        out = {}
+        for k in z.files:
+            case, field = k.split("/", 1)
+            out.setdefault(case, {})[field] = z[k]
+        _CACHE[fname] = out
+    return _CACHE[fname]
+
+
+def case_args(rec):
+    """Reference-style arguments of a filter golden case."""
+    model = str(rec["model"]).lower()
+    if "beta" in rec:
+        theta = (rec["beta"], float(rec["gamma"]))
+        npop, mu = rec["npop"], rec["mu"]
+    else:
+        theta = rec["theta"]
+        npop, mu = float(rec["npop"][0]), float(rec["mu"][0])
+    return dict(Y=rec["Y"], model=model, theta=theta, observations=bool(rec["obs"]), probs=float(rec["probs"]),
+                N=int(rec["N"]), npop=npop, mu=mu, key=int(rec["key"]), f=int(rec["f"]))
+
+
+@pytest.fixture(scope="session")
+def filter_golden():
+    return load_golden("filter_golden.npz")
+
+
+@pytest.fixture(scope="session")
+def kernels_golden():
+    return load_golden("kernels_golden.npz")
+
+
+@pytest.fixture(scope="session")
+def pmcmc_golden():
+    return load_golden("pmcmc_golden.npz")
+
+
+@pytest.fixture(scope="session")
+def datasets_golden():
+    z = np.load(os.path.join(GOLDEN, "datasets.npz"), allow_pickle=False)
+    return {k: z[k] for k in z.files}

@@ -1,0 +1,415 @@
+"""Generate the golden fixtures in tests/golden/ by running the UNMODIFIED reference.
+
+Runs only in the build container (the reference is never shipped; /root/reference does not exist
+on the GPU box).  Usage:  python tests/golden/make_golden.py [--reference /root/reference]
+
+How the reference is driven (SURVEY.md §8c "RNG-injection shim"):
+  * `gillespie_algo.np` and `pmcmc.np` are replaced by a proxy module whose `random` attribute
+    intercepts exactly three calls and forwards everything else to numpy's real global RandomState:
+      - `np.random.exponential(scale)`  (gillespie_algo.py:62,133,208): tau = scale * (-log(1 - U1))
+        with U1 from the keyed Philox stream (oracle/philox.py).  The identity with numpy's legacy
+        exponential is asserted below on a real MT19937 stream before any fixture is written.
+      - `np.random.choice(...)`         (gillespie_algo.py:63,134,209 and pmcmc.py:188): numpy's OWN
+        legacy `RandomState.choice` runs, on a RandomState subclass whose `random_sample` returns the
+        keyed uniforms -- so validation, cumsum, normalisation and searchsorted are numpy's code.
+      - `np.random.poisson(mu, N)`      (pmcmc.py:157,161,167): inversion on the keyed stream (the
+        stream's definition of the initial draw; numpy's PTRS cannot run on a counter stream).
+  * `pmcmc.sir_simulate` / `seir_simulate` / `sir_subgroups_simulate` are wrapped to learn the
+    (step p, particle j) of each call from the call order (jobs=1 calls them in order), and
+    `pmcmc.particle_filter` is wrapped to assign one filter index per call.
+  * `pmcmc.Parallel` is replaced by an in-process loop (jobs=1 already runs sequentially).
+MH proposals (`multivariate_normal`), acceptance uniforms and the path sampler's `randint` stay on
+numpy's real global RandomState, seeded with `np.random.seed(seed)`, exactly as in the reference.
+
+Datasets are synthesised with the reference's own recipes (pmcmc.py:54-113 ODE integrators plus the
+binomial-thinning / Gaussian-noise loops quoted in tests/test_pmcmc_p.py:21-29,
+tests/test_pmcmc_noisy.py:21-29, tests/test_simulations_subgroups.py:57-64) BEFORE the shim is
+installed, on seeded RandomStates.
+"""
+import argparse
+import math
+import os
+import sys
+import time
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import philox as ph  # noqa: E402
+
+
+# ----------------------------------------------------------------------------------- shim
+class _Stream:
+    key = 0
+    next_f = 0
+    f = 0
+    N = 1
+    ssa_calls = 0
+    resamples = 0
+    poissons = 0
+    p = 0
+    j = 0
+    k = 0
+    u2 = None
+    direct = False  # direct SSA call: (p, j) set by the caller
+
+
+S = _Stream()
+
+
+class _Injected(np.random.RandomState):
+    """numpy's legacy RandomState with `random_sample` answered from a preset array."""
+
+    def __init__(self):
+        super().__init__(0)
+        self.u = None
+
+    def random_sample(self, size=None):
+        if size is None:
+            return float(self.u)
+        return np.asarray(self.u, dtype=np.float64).reshape(size)
+
+
+_INJ = _Injected()
+
+
+class _RandomProxy:
+    def __getattr__(self, name):
+        return getattr(np.random, name)
+
+    def exponential(self, scale=1.0, size=None):
+        assert size is None
+        u1, u2 = ph.ssa_uniforms(S.key, S.f, S.p, S.j, S.k)
+        S.k += 1
+        S.u2 = float(u2)
+        return scale * (-math.log(1.0 - float(u1)))
+
+    def choice(self, a, size=None, replace=True, p=None):
+        if size is None:  # SSA channel choice: the second uniform of the current event block
+            assert S.u2 is not None
+            _INJ.u = S.u2
+            S.u2 = None
+            return _INJ.choice(a, size, replace, p)
+        S.resamples += 1  # multinomial resample at step p = resamples
+        _INJ.u = ph.resample_uniforms(S.key, S.f, S.resamples, int(size))
+        return _INJ.choice(a, size, replace, p)
+
+    def poisson(self, lam=1.0, size=None):
+        g = S.poissons
+        S.poissons += 1
+        u = ph.init_uniforms(S.key, S.f, g, int(size))
+        return ph.poisson_inversion(u, float(lam)).astype(np.float64)
+
+
+class _NpProxy(types.ModuleType):
+    def __getattr__(self, name):
+        return getattr(np, name)
+
+
+class _SeqParallel:
+    def __init__(self, n_jobs=None, **kw):
+        pass
+
+    def __call__(self, it):
+        return [f(*a, **k) for f, a, k in it]
+
+
+def _wrap_ssa(fn):
+    def w(*args, **kw):
+        if not S.direct:
+            c = S.ssa_calls
+            S.ssa_calls += 1
+            S.p = c // S.N + 1
+            S.j = c % S.N
+        S.k = 0
+        S.u2 = None
+        return fn(*args, **kw)
+
+    return w
+
+
+def install_shim(pm, ga):
+    npx = _NpProxy("numpy_keyed_proxy")
+    npx.random = _RandomProxy()
+    pm.np = npx
+    ga.np = npx
+    pm.Parallel = _SeqParallel
+    for name in ("sir_simulate", "seir_simulate", "sir_subgroups_simulate"):
+        setattr(pm, name, _wrap_ssa(getattr(ga, name)))
+    orig_pf = pm.particle_filter
+
+    def pf(Y, type_model, theta_proposal, observations=False, probs=0.1, n_particles=1000, n_population=4820,
+           mu=20, jobs=4):
+        S.f = S.next_f
+        S.next_f += 1
+        S.N = int(n_particles)
+        S.ssa_calls = S.resamples = S.poissons = 0
+        S.direct = False
+        return orig_pf(Y, type_model, theta_proposal, observations, probs, n_particles, n_population, mu, 1)
+
+    pm.particle_filter = pf
+    return pf
+
+
+def check_numpy_identities():
+    """Assert the two numpy-legacy identities the shim relies on, on a real MT19937 stream."""
+    rs = np.random.RandomState(12345)
+    st = rs.get_state()
+    e = [rs.exponential(s) for s in np.linspace(0.01, 3.0, 20000)]
+    rs.set_state(st)
+    u = [rs.random_sample() for _ in range(20000)]
+    for s, ei, ui in zip(np.linspace(0.01, 3.0, 20000), e, u):
+        assert ei == s * (-math.log(1.0 - ui)), "legacy exponential identity broken"
+    rs = np.random.RandomState(7)
+    for n in (2, 3, 6, 17, 200):
+        for _ in range(50):
+            w = rs.random_sample(n) * (rs.random_sample(n) > 0.2)
+            if w.sum() == 0:
+                continue
+            st = rs.get_state()
+            a = rs.choice(range(n), n, p=w / sum(w))
+            rs.set_state(st)
+            uu = rs.random_sample(n)
+            _INJ.u = uu
+            b = _INJ.choice(range(n), n, p=w / sum(w))
+            assert np.array_equal(a, b), "injected choice differs from numpy's"
+
+
+# ----------------------------------------------------------------------------------- datasets
+def thin_binomial(values, prob, rs):
+    """tests/test_pmcmc_p.py:21-29 / tests/test_simulations_subgroups.py:57-64 recipe."""
+    out = []
+    for row in values:
+        out.append([rs.binomial(v, prob) for v in row])
+    return np.array(out, dtype=np.float64)
+
+
+def noise_normal(values, ratio, rs):
+    """tests/test_pmcmc_noisy.py:21-29 recipe (Gaussian noise, cast to int)."""
+    out = []
+    for row in values:
+        out.append([rs.normal(v, ratio * v) for v in row])
+    return np.array(out).astype(int).astype(np.float64)
+
+
+def make_datasets(pm):
+    d = {}
+    sir = pm.sir_simulate_discrete((4800, 20, 0), np.linspace(0, 14, num=200), 2, 1)
+    d["sir_ode"] = sir.iloc[:, 1:4].to_numpy(dtype=np.float64)
+    d["sir_binom"] = thin_binomial(d["sir_ode"], 0.1, np.random.RandomState(11))
+    d["sir_noisy"] = noise_normal(d["sir_ode"], 0.1, np.random.RandomState(12))
+    seir = pm.seir_simulate_discrete((4800, 0, 20, 0), np.linspace(0, 10, num=200), 4, 1, 1)
+    d["seir_ode"] = seir.iloc[:, 1:5].to_numpy(dtype=np.float64)
+    d["seir_binom"] = thin_binomial(d["seir_ode"], 0.1, np.random.RandomState(13))
+    pop = np.array([[2000, 30, 0], [3000, 40, 0]])
+    beta = np.array([[5, 2], [1, 3]])
+    sub = pm.sir_subgroups_simulate_discrete(pop, np.linspace(0, 14, num=200), beta, 0.5)
+    d["sub_ode"] = sub.iloc[:, 0:6].to_numpy(dtype=np.float64)
+    d["sub_binom"] = thin_binomial(d["sub_ode"], 0.1, np.random.RandomState(14))
+    d["sub2_binom"] = d["sub_binom"][:, 0:3] + d["sub_binom"][:, 3:6]
+    small = pm.sir_simulate_discrete((180, 20, 0), np.linspace(0, 49, num=500), 2, 1)
+    d["cfg1_ode"] = small.iloc[:, 1:4].to_numpy(dtype=np.float64)
+    d["cfg1_binom"] = thin_binomial(d["cfg1_ode"], 0.1, np.random.RandomState(2))
+    c2 = pm.sir_simulate_discrete((9980, 20, 0), np.linspace(0, 199, num=2000), 0.25, 0.1)
+    d["cfg2_ode"] = c2.iloc[:, 1:4].to_numpy(dtype=np.float64)
+    d["cfg2_binom"] = thin_binomial(d["cfg2_ode"], 0.1, np.random.RandomState(1))
+    c3 = pm.seir_simulate_discrete((9980, 0, 20, 0), np.linspace(0, 199, num=2000), 0.5, 0.2, 0.1)
+    d["cfg3_ode"] = c3.iloc[:, 1:5].to_numpy(dtype=np.float64)
+    d["cfg3_noisy"] = noise_normal(d["cfg3_ode"], 0.1, np.random.RandomState(3))
+    return d
+
+
+# ----------------------------------------------------------------------------------- cases
+FILTER_CASES = [
+    # name, model, dataset, theta, observations, probs, N, npop, mu, key, rows
+    ("sir_binom", "SIR", "sir_binom", (2.0, 1.0), False, 0.1, 24, 4820, 20, 1001, None),
+    ("sir_normal", "SIR", "sir_noisy", (2.0, 1.0), True, 0.5, 16, 4820, 20, 1002, None),
+    ("seir_binom", "SEIR", "seir_binom", (4.0, 1.0, 1.0), False, 0.1, 10, 4820, 20, 1003, None),
+    ("sub_binom", "SIR_SUBGROUPS", "sub_binom", "sub", False, 0.1, 8, [2030, 3040], [30, 40], 1004, 7),
+    ("sub2_binom", "SIR_SUBGROUPS2", "sub2_binom", "sub", False, 0.1, 8, [2030, 3040], [30, 40], 1005, 7),
+    ("cfg1_sir", "SIR", "cfg1_binom", (2.0, 1.0), False, 0.1, 100, 200, 20, 1006, None),
+    ("cfg2_sir", "SIR", "cfg2_binom", (0.25, 0.1), False, 0.1, 6, 10000, 20, 1007, None),
+    ("cfg3_seir_normal", "SEIR", "cfg3_noisy", (0.5, 0.2, 0.1), True, 0.1, 4, 10000, 20, 1008, 60),
+    ("sir_theta_off", "SIR", "sir_binom", (2.3, 0.9), False, 0.1, 20, 4820, 20, 1009, None),
+    ("degenerate", "SIR", "degenerate", (2.0, 1.0), False, 0.1, 12, 4820, 20, 1010, None),
+]
+
+SUB_THETA = (np.array([[5.0, 2.0], [1.0, 3.0]]), 0.5)
+
+
+def run_filter_cases(pm, pf, d, out):
+    for name, model, ds, theta, obs, probs, N, npop, mu, key, rows in FILTER_CASES:
+        Y = d[ds] if ds != "degenerate" else d["sir_binom"].copy()
+        if ds == "degenerate":
+            Y[3, 0] = 5000.0  # more observed susceptibles than people: every weight 0 at step 4
+        if rows:
+            Y = Y[:rows]
+        th = SUB_THETA if theta == "sub" else np.array(theta)
+        S.key = key
+        S.next_f = 0
+        t0 = time.time()
+        z, hid, anc = pf(Y, getattr(pm.ModelType, model), th, obs, probs, N,
+                         np.array(npop) if isinstance(npop, list) else npop,
+                         np.array(mu) if isinstance(mu, list) else mu, 1)
+        dt = time.time() - t0
+        rec = dict(Y=Y, model=model, obs=obs, probs=probs, N=N, npop=np.atleast_1d(npop).astype(float),
+                   mu=np.atleast_1d(mu).astype(float), key=key, f=0, seconds=dt)
+        if theta == "sub":
+            rec["beta"], rec["gamma"] = SUB_THETA
+        else:
+            rec["theta"] = th
+        if z is None:
+            rec["status"] = 1
+        else:
+            rec.update(status=0, zetas=z, hidden=hid.astype(np.int32), ancestry=anc.astype(np.int32))
+            assert np.array_equal(hid, np.round(hid)) and np.array_equal(anc, np.round(anc))
+        out["filter_" + name] = rec
+        print(f"filter {name}: status={rec['status']} {dt:.2f}s", flush=True)
+
+
+def run_ssa_cases(pm, ga, out):
+    rs = np.random.RandomState(21)
+    cases = []
+    st = np.stack([4820 - rs.randint(1, 400, 24), rs.randint(1, 400, 24), np.zeros(24, int)], 1)
+    st[:, 2] = rs.randint(0, 200, 24)
+    st[:, 0] -= st[:, 2]
+    cases.append(("sir", ga.sir_simulate, st, (2.0, 1.0)))
+    st2 = np.array([[10, 0, 0], [10, 1, 0], [5, 0, 5], [0, 3, 7], [100, 0, 0]])
+    cases.append(("sir_edge", ga.sir_simulate, st2, (1.5, 0.5)))
+    se = np.stack([4800 - rs.randint(0, 300, 12), rs.randint(0, 100, 12), rs.randint(1, 100, 12),
+                   np.zeros(12, int)], 1)
+    se[0, 2] = 0  # E>0, I=0 start
+    cases.append(("seir", ga.seir_simulate, se, (4.0, 1.0, 1.0)))
+    sg = np.stack([2000 - rs.randint(0, 200, 10), rs.randint(0, 60, 10), np.zeros(10, int),
+                   3000 - rs.randint(0, 200, 10), rs.randint(0, 60, 10), np.zeros(10, int)], 1)
+    sg[0, 1] = 0
+    cases.append(("sub", ga.sir_subgroups_simulate, sg, "sub"))
+    for name, fn, states, theta in cases:
+        for max_time in (1.0, 2.5):
+            S.direct = True
+            S.key = 77
+            S.f = 5
+            res = []
+            for j, x in enumerate(states):
+                S.p, S.j = 3, j
+                S.k = 0
+                if theta == "sub":
+                    r = fn(x.reshape(2, 3).astype(float), SUB_THETA[0], SUB_THETA[1], max_time, True)
+                    res.append([v for g in r for v in g])
+                else:
+                    r = fn(list(x.astype(float)), np.array(theta), max_time, True)
+                    res.append(list(r))
+            S.direct = False
+            out[f"ssa_{name}_{max_time}"] = dict(states=states.astype(np.int32), theta=np.array(
+                [5.0, 2.0, 1.0, 3.0, 0.5]) if theta == "sub" else np.array(theta), max_time=max_time, key=77, f=5,
+                step=3, out=np.array(res).astype(np.int32), model=name.split("_")[0])
+
+
+def run_resample_cases(out):
+    rs = np.random.RandomState(31)
+    for n in (1, 2, 5, 64, 257, 1000):
+        w = rs.random_sample(n) ** 3
+        w[rs.random_sample(n) < 0.3] = 0.0
+        if n > 1:
+            w[0] = 0.0
+            w[-1] = 0.0
+        if w.sum() == 0:
+            w[n // 2] = 1.0
+        st = rs.get_state()
+        exp = rs.choice(range(n), n, p=w / sum(w))
+        rs.set_state(st)
+        u = rs.random_sample(n)
+        out[f"resample_{n}"] = dict(w=w, u=u, expected=np.asarray(exp, dtype=np.int32))
+
+
+def run_pmf_cases(out):
+    from scipy.stats import binom, norm
+    rs = np.random.RandomState(41)
+    n = rs.randint(0, 10001, 4000).astype(float)
+    k = np.floor(rs.random_sample(4000) * (n + 1) * rs.choice([0.05, 0.2, 1.0, 1.3], 4000))
+    p = rs.choice([0.0, 1.0, 0.1, 0.05, 0.5, 0.999, 1e-3], 4000)
+    out["pmf_binom"] = dict(k=k, n=n, p=p, pmf=binom.pmf(k, n, p))
+    y = rs.randint(0, 3000, 2000).astype(float)
+    x = np.maximum(0, y + rs.normal(0, 200, 2000)).round()
+    pr = rs.choice([0.1, 0.5, 0.01], 2000)
+    out["pdf_normal"] = dict(y=y, x=x, probs=pr, pdf=norm.pdf(y, x, pr * x + .0001))
+
+
+PMCMC_CASES = [
+    # name, model, dataset, rows, params, h, sigma, iters, probs, N, npop, mu, adaptive, seed, key
+    ("sir_small", "SIR", "cfg1_binom", 30, [2.0, 1.0], 0.01, None, 25, 0.1, 20, 200, 20, False, 7, 2001),
+    ("sir_p", "SIR", "sir_binom", None, [2.0, 1.0, 0.1], 1.0, np.diag([4e-3, 2e-3, 1e-5]), 12, None, 12, 4820, 20,
+     False, 8, 2002),
+    ("sub", "SIR_SUBGROUPS", "sub_binom", 6, [4.0, 1.0, 1.0, 4.0, 1.0], 0.05, None, 6, 0.1, 6, [2030, 3040],
+     [30, 40], False, 9, 2003),
+    ("sir_adaptive", "SIR", "cfg1_binom", 10, [2.0, 1.0], 0.01, None, 1030, 0.1, 6, 200, 20, True, 10, 2004),
+]
+
+
+def run_pmcmc_cases(pm, d, out):
+    for name, model, ds, rows, params, h, sigma, iters, probs, N, npop, mu, adaptive, seed, key in PMCMC_CASES:
+        Y = d[ds] if rows is None else d[ds][:rows]
+        S.key = key
+        S.next_f = 0
+        np.random.seed(seed)
+        t0 = time.time()
+        th, lk, tr = pm.particle_mcmc(Y, getattr(pm.ModelType, model), list(params), h, adaptive=adaptive,
+                                      sigma=sigma, n_chains=iters, observations=False, probs=probs, n_particles=N,
+                                      n_population=np.array(npop) if isinstance(npop, list) else npop,
+                                      mu=np.array(mu) if isinstance(mu, list) else mu, jobs=1)
+        dt = time.time() - t0
+        out["pmcmc_" + name] = dict(Y=Y, model=model, params=np.array(params), h=h,
+                                    sigma=np.zeros((0, 0)) if sigma is None else sigma, iters=iters,
+                                    probs=-1.0 if probs is None else probs, N=N,
+                                    npop=np.atleast_1d(npop).astype(float), mu=np.atleast_1d(mu).astype(float),
+                                    adaptive=adaptive, seed=seed, key=key, n_filters=S.next_f, thetas=th,
+                                    likelihoods=lk, trajs=tr, seconds=dt)
+        print(f"pmcmc {name}: {dt:.1f}s filters={S.next_f}", flush=True)
+
+
+def save(out, path):
+    flat = {}
+    for case, rec in out.items():
+        for k, v in rec.items():
+            flat[f"{case}/{k}"] = np.asarray(v)
+    np.savez_compressed(path, **flat)
+    print("wrote", path, len(flat), "arrays")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reference", default="/root/reference")
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    sys.path.insert(0, args.reference)
+    import matplotlib
+    matplotlib.use("Agg")
+    import gillespie_algo as ga
+    import pmcmc as pm
+
+    check_numpy_identities()
+    d = make_datasets(pm)
+    np.savez_compressed(os.path.join(HERE, "datasets.npz"), **d)
+    pf = install_shim(pm, ga)
+    only = set(args.only.split(",")) if args.only else None
+    if not only or "filter" in only:
+        out = {}
+        run_filter_cases(pm, pf, d, out)
+        save(out, os.path.join(HERE, "filter_golden.npz"))
+    if not only or "ssa" in only:
+        out = {}
+        run_ssa_cases(pm, ga, out)
+        run_resample_cases(out)
+        run_pmf_cases(out)
+        save(out, os.path.join(HERE, "kernels_golden.npz"))
+    if not only or "pmcmc" in only:
+        out = {}
+        run_pmcmc_cases(pm, d, out)
+        save(out, os.path.join(HERE, "pmcmc_golden.npz"))
+
+
+if __name__ == "__main__":
+    main()

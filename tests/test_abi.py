@@ -1,0 +1,63 @@
+"""The C-ABI library loads and exports every entry point include/epipf.h declares (CPU-safe: no
+compute calls, no device needed)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import PKG, REPO
+
+HEADER = os.path.join(REPO, "include", "epipf.h")
+LIB = os.path.join(PKG, "lib", "libepipf.so")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(epipf_[a-z_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    syms = declared_symbols()
+    for s in ("epipf_create", "epipf_run", "epipf_path_sample", "epipf_simulate", "epipf_resample"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    assert os.path.exists(LIB), "run __graft_entry__.build() first"
+    L = ctypes.CDLL(LIB)
+    missing = [s for s in declared_symbols() if not hasattr(L, s)]
+    assert not missing, missing
+
+
+def test_python_binding_lists_every_symbol():
+    from epipf import _lib
+    assert sorted(_lib.EXPORTS) == declared_symbols()
+
+
+def test_abi_version_and_device_query():
+    from epipf import _lib
+    L = _lib.load()
+    assert L.epipf_abi_version() == _lib.ABI_VERSION
+    assert L.epipf_device_count() >= 0
+
+
+def test_create_without_device_fails_loudly():
+    """No CPU fallback: on a GPU-less host the engine refuses to construct."""
+    from epipf import _lib
+    from epipf.engine import Engine
+    if _lib.load().epipf_device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(_lib.EpipfError):
+        Engine("sir", 1, 16, 4, 1)
+
+
+def test_constants_match_header():
+    from epipf import _lib
+    text = open(HEADER).read()
+    defs = dict(re.findall(r"#define (EPIPF_\w+) \(?(-?\d+)\)?", text))
+    assert int(defs["EPIPF_STATUS_DEGENERATE"]) == _lib.STATUS_DEGENERATE
+    assert int(defs["EPIPF_SIR_SUBGROUPS2"]) == _lib.SIR_SUBGROUPS2
+    assert int(defs["EPIPF_RESAMPLE_SYSTEMATIC"]) == _lib.RESAMPLE_SYSTEMATIC
+    assert int(defs["EPIPF_ABI_VERSION"]) == _lib.ABI_VERSION

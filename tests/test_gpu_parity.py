@@ -1,0 +1,298 @@
+"""Parity of the HIP path (libepipf.so through its C ABI) with the reference golden vectors and the
+CPU oracle.  Integer outputs (states, ancestors, trajectories) must be bit-exact; log-likelihoods
+within 1e-9 absolute (1e-6 relative is the north-star bound).  Needs an MI355X: `-m gpu`."""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import case_args
+
+pytestmark = pytest.mark.gpu
+
+FILTER_CASES = ["sir_binom", "sir_normal", "seir_binom", "sub_binom", "sub2_binom", "cfg1_sir", "cfg2_sir",
+                "cfg3_seir_normal", "sir_theta_off", "degenerate"]
+
+
+def engine_for(a, chains=1):
+    from epipf.engine import get_engine, model_id, theta_vector
+    mid = model_id(a["model"])
+    th, G = theta_vector(mid, a["theta"])
+    eng = get_engine(mid, G, a["N"], a["Y"].shape[0], chains)
+    eng.set_observations(a["Y"])
+    eng.set_population(a["npop"], a["mu"])
+    return eng, th
+
+
+@pytest.mark.parametrize("name", FILTER_CASES)
+def test_filter_matches_reference_golden(filter_golden, name):
+    rec = filter_golden["filter_" + name]
+    a = case_args(rec)
+    eng, th = engine_for(a)
+    lz, st = eng.run(th[None], [a["probs"]], [a["key"]], [a["f"]], observations=a["observations"])
+    assert int(st[0]) == int(rec["status"])
+    if st[0]:
+        return
+    hid, anc = eng.history(1)
+    np.testing.assert_array_equal(hid[0], rec["hidden"])
+    np.testing.assert_array_equal(anc[0], rec["ancestry"])
+    z = rec["zetas"]
+    ok = z > 1e-290
+    np.testing.assert_allclose(lz[0][ok], np.log(z[ok]), rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("name", FILTER_CASES)
+def test_filter_matches_oracle(filter_golden, name):
+    rec = filter_golden["filter_" + name]
+    a = case_args(rec)
+    eng, th = engine_for(a)
+    lz, st = eng.run(th[None], [a["probs"]], [a["key"]], [a["f"]], observations=a["observations"])
+    o = oracle.particle_filter(a["Y"], a["model"], a["theta"], a["observations"], a["probs"], a["N"], a["npop"],
+                               a["mu"], key=a["key"], filter_index=a["f"])
+    assert int(st[0]) == o["status"]
+    if o["status"]:
+        return
+    hid, anc = eng.history(1)
+    np.testing.assert_array_equal(hid[0], o["hidden"])
+    np.testing.assert_array_equal(anc[0], o["ancestry"])
+    np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_filter_random_configs_vs_oracle(datasets_golden, seed):
+    """Seeded random (theta, N, key) on every model: bit-exact states/ancestors vs the oracle."""
+    rs = np.random.RandomState(100 + seed)
+    model = ["sir", "seir", "sir_subgroups", "sir_subgroups2", "sir", "seir"][seed]
+    obs = bool(seed >= 4)
+    N = int(rs.choice([1, 7, 64, 65, 300, 1000]))
+    if model == "sir":
+        Y, th, npop, mu = datasets_golden["sir_noisy" if obs else "sir_binom"], rs.uniform(1.5, 2.5, 2) * [1, .5], 4820, 20
+        probs = 0.5 if obs else 0.1
+    elif model == "seir":
+        Y, th, npop, mu = datasets_golden["seir_binom"], rs.uniform(0.8, 1.2, 3) * [4, 1, 1], 4820, 20
+        probs = 0.3 if obs else 0.1
+    else:
+        Y = datasets_golden["sub_binom" if model == "sir_subgroups" else "sub2_binom"][:6]
+        th = (np.array([[5, 2], [1, 3]]) * rs.uniform(0.8, 1.2, (2, 2)), 0.5)
+        npop, mu, probs = np.array([2030., 3040.]), np.array([30., 40.]), 0.1
+        N = min(N, 300)
+    a = dict(Y=Y, model=model, theta=th, observations=obs, probs=probs, N=N, npop=npop, mu=mu,
+             key=int(rs.randint(1, 2**31)), f=int(rs.randint(0, 1000)))
+    eng, thv = engine_for(a)
+    lz, st = eng.run(thv[None], [probs], [a["key"]], [a["f"]], observations=obs)
+    o = oracle.particle_filter(Y, model, th, obs, probs, N, npop, mu, key=a["key"], filter_index=a["f"])
+    assert int(st[0]) == o["status"]
+    if o["status"]:
+        return
+    hid, anc = eng.history(1)
+    np.testing.assert_array_equal(hid[0], o["hidden"])
+    np.testing.assert_array_equal(anc[0], o["ancestry"])
+    np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
+def test_batched_chains_equal_single_runs(datasets_golden):
+    """Chain c of a batched launch is bit-identical to running it alone (no cross-chain coupling),
+    and inactive chains are skipped."""
+    Y = datasets_golden["sir_binom"]
+    a = dict(Y=Y, model="sir", theta=(2.0, 1.0), N=200, npop=4820, mu=20)
+    eng, _ = engine_for(a, chains=5)
+    thetas = np.array([[2.0, 1.0], [2.2, 0.9], [1.8, 1.1], [2.0, 1.0], [2.5, 1.3]])
+    keys = np.array([11, 12, 13, 14, 15], dtype=np.uint64)
+    fidx = np.array([0, 3, 5, 7, 9])
+    act = np.array([1, 1, 0, 1, 1])
+    lz, st = eng.run(thetas, 0.1, keys, fidx, active=act)
+    assert list(st) == [0, 0, 2, 0, 0]
+    hid, anc = eng.history(5)
+    for c in (0, 1, 3, 4):
+        o = oracle.particle_filter(Y, "sir", thetas[c], False, 0.1, 200, 4820, 20, key=int(keys[c]),
+                                   filter_index=int(fidx[c]))
+        np.testing.assert_array_equal(hid[c], o["hidden"])
+        np.testing.assert_array_equal(anc[c], o["ancestry"])
+        np.testing.assert_allclose(lz[c], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
+def test_deterministic_reruns(datasets_golden):
+    Y = datasets_golden["cfg2_binom"]
+    a = dict(Y=Y, model="sir", theta=(0.25, 0.1), N=2000, npop=10000, mu=20)
+    eng, th = engine_for(a)
+    r1 = eng.run(th[None], 0.1, 7, 1)
+    h1 = eng.history(1)
+    r2 = eng.run(th[None], 0.1, 7, 1)
+    h2 = eng.history(1)
+    np.testing.assert_array_equal(r1[0], r2[0])
+    np.testing.assert_array_equal(h1[0], h2[0])
+    np.testing.assert_array_equal(h1[1], h2[1])
+
+
+@pytest.mark.parametrize("name", ["sir_1.0", "sir_2.5", "sir_edge_1.0", "sir_edge_2.5", "seir_1.0", "seir_2.5",
+                                  "sub_1.0", "sub_2.5"])
+def test_simulate_matches_reference_golden(kernels_golden, name):
+    from epipf import simulate_batch
+    rec = kernels_golden["ssa_" + name]
+    model = str(rec["model"])
+    theta = (rec["theta"][:4].reshape(2, 2), float(rec["theta"][4])) if model == "sub" else rec["theta"]
+    mname = {"sir": "sir", "seir": "seir", "sub": "sir_subgroups"}[model]
+    out, _ = simulate_batch(mname, rec["states"], theta, float(rec["max_time"]), key=int(rec["key"]),
+                            filter_index=int(rec["f"]), step=int(rec["step"]))
+    np.testing.assert_array_equal(out, rec["out"])
+
+
+def test_simulate_large_batch_vs_oracle():
+    from epipf import simulate_batch
+    rs = np.random.RandomState(3)
+    n = 20000
+    I = rs.randint(0, 500, n)
+    R = rs.randint(0, 500, n)
+    st = np.stack([10000 - I - R, I, R], 1)
+    out, ev = simulate_batch("sir", st, (0.25, 0.1), 3.0, key=123, filter_index=4, step=9)
+    o, oev = oracle.simulate("sir", st, (0.25, 0.1), 3.0, 123, 4, 9)
+    np.testing.assert_array_equal(out, o)
+    assert ev == oev
+    np.testing.assert_array_equal(out.sum(1), 10000)  # conservation
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 64, 257, 1000])
+def test_resample_matches_numpy_choice(kernels_golden, n):
+    from epipf.engine import get_engine
+    rec = kernels_golden[f"resample_{n}"]
+    eng = get_engine("sir", 1, 8, 2, 1)
+    out, _ = eng.resample(rec["w"], rec["u"])
+    np.testing.assert_array_equal(out, rec["expected"])
+
+
+def test_resample_ties_take_the_exact_path():
+    """Uniforms placed exactly on (and one ulp around) numpy's CDF boundaries: the certified search must
+    hand them to the sequential path and still equal numpy's answer."""
+    from epipf.engine import get_engine
+    eng = get_engine("sir", 1, 8, 2, 1)
+    rs = np.random.RandomState(5)
+    n = 3000
+    w = rs.random_sample(n) ** 4
+    w[rs.random_sample(n) < 0.2] = 0.0
+    p = w / sum(w)
+    cdf = p.cumsum()
+    cdf /= cdf[-1]
+    idx = rs.randint(0, n - 1, 300)
+    u = np.concatenate([cdf[idx], np.nextafter(cdf[idx], 0), np.nextafter(cdf[idx], 1), rs.random_sample(100)])
+    u = np.resize(u[(u >= 0) & (u < 1)], n)
+    out, fb = eng.resample(w, u)
+    np.testing.assert_array_equal(out, oracle.resample(w, u))
+    assert fb > 0
+
+
+def test_resample_degenerate_weights():
+    from epipf.engine import get_engine
+    eng = get_engine("sir", 1, 8, 2, 1)
+    out, _ = eng.resample(np.zeros(100), np.full(100, 0.5))
+    assert out is None
+
+
+def test_path_sampler_matches_host_version(filter_golden):
+    from epipf import particle_path_sampler
+    rec = filter_golden["filter_sir_binom"]
+    a = case_args(rec)
+    eng, th = engine_for(a)
+    eng.run(th[None], [a["probs"]], [a["key"]], [a["f"]])
+    hid, anc = eng.history(1)
+    for chosen in (0, 5, a["N"] - 1):
+        dev = eng.path_sample([chosen])[0]
+        np.random.seed(0)
+        # host reference implementation with the same pick
+        traj = np.zeros((hid.shape[1], hid.shape[3]))
+        traj[-1] = hid[0, -1, chosen]
+        c = chosen
+        for p in range(hid.shape[1] - 2, -1, -1):
+            c = int(anc[0, p, c])
+            traj[p] = hid[0, p, c]
+        np.testing.assert_array_equal(dev, traj)
+    np.random.seed(3)
+    host = particle_path_sampler(hid[0].astype(float), anc[0].astype(float))
+    np.random.seed(3)
+    dev = eng.path_sample([np.random.randint(0, a["N"])])[0]
+    np.testing.assert_array_equal(dev, host)
+
+
+def test_dropin_particle_filter_signature(filter_golden):
+    from epipf import ModelType, particle_filter, seed_stream
+    rec = filter_golden["filter_seir_binom"]
+    a = case_args(rec)
+    seed_stream(a["key"], a["f"])
+    z, hid, anc = particle_filter(a["Y"], ModelType.SEIR, np.array(a["theta"]), False, a["probs"], a["N"],
+                                  a["npop"], a["mu"], jobs=-1)
+    np.testing.assert_array_equal(hid, rec["hidden"].astype(float))
+    np.testing.assert_array_equal(anc, rec["ancestry"].astype(float))
+    np.testing.assert_allclose(z, rec["zetas"], rtol=1e-9)
+    assert hid.dtype == np.float64 and anc.dtype == np.float64
+    rec = filter_golden["filter_degenerate"]
+    a = case_args(rec)
+    assert particle_filter(a["Y"], "sir", a["theta"], n_particles=a["N"], key=a["key"], filter_index=0) == \
+        (None, None, None)
+
+
+@pytest.mark.parametrize("name", ["sir_small", "sir_p", "sub", "sir_adaptive"])
+def test_pmcmc_matches_reference_golden(pmcmc_golden, name):
+    """particle_mcmc under np.random.seed(s) + seed_stream(key): identical accept/reject trace, thetas,
+    sampled trajectories; likelihoods within 1e-9 relative."""
+    from epipf import particle_mcmc, seed_stream
+    rec = pmcmc_golden["pmcmc_" + name]
+    model = str(rec["model"])
+    G = len(rec["npop"])
+    npop = rec["npop"] if model.startswith("SIR_SUB") else float(rec["npop"][0])
+    mu = rec["mu"] if model.startswith("SIR_SUB") else float(rec["mu"][0])
+    sigma = None if rec["sigma"].size == 0 else rec["sigma"]
+    probs = None if float(rec["probs"]) < 0 else float(rec["probs"])
+    seed_stream(int(rec["key"]), 0)
+    np.random.seed(int(rec["seed"]))
+    th, lk, tr = particle_mcmc(rec["Y"], model.lower(), list(rec["params"]), float(rec["h"]),
+                               adaptive=bool(rec["adaptive"]), sigma=sigma, n_chains=int(rec["iters"]),
+                               probs=probs, n_particles=int(rec["N"]), n_population=npop, mu=mu, progress=False)
+    assert G >= 1
+    np.testing.assert_array_equal(th, rec["thetas"])
+    np.testing.assert_array_equal(tr, rec["trajs"])
+    np.testing.assert_allclose(lk, rec["likelihoods"], rtol=1e-9)
+
+
+def test_multichain_equals_single_chain(datasets_golden):
+    from epipf import particle_mcmc_chains
+    Y = datasets_golden["cfg1_binom"][:20]
+    kw = dict(Y=Y, type_model="sir", parameters=[2.0, 1.0], h=0.01, n_chains=15, probs=0.1, n_particles=64,
+              n_population=200, mu=20, mh_ratio="log")
+    multi = particle_mcmc_chains(**kw, chains=4, seed=21)
+    for c in range(4):
+        single = particle_mcmc_chains(**kw, rngs=[np.random.RandomState(21 + c)],
+                                      keys=[multi_key(21, c)])[0]
+        np.testing.assert_array_equal(single.thetas, multi[c].thetas)
+        np.testing.assert_array_equal(single.sampled_trajs, multi[c].sampled_trajs)
+
+
+def multi_key(seed, c):
+    from epipf import chain_key
+    return chain_key(seed, c)
+
+
+def test_systematic_resampling_vs_oracle(datasets_golden):
+    Y = datasets_golden["sir_binom"]
+    a = dict(Y=Y, model="sir", theta=(2.0, 1.0), N=500, npop=4820, mu=20)
+    eng, th = engine_for(a)
+    lz, st = eng.run(th[None], 0.1, 77, 2, resample="systematic")
+    o = oracle.particle_filter(Y, "sir", (2.0, 1.0), False, 0.1, 500, 4820, 20, key=77, filter_index=2,
+                               resample="systematic")
+    hid, anc = eng.history(1)
+    np.testing.assert_array_equal(anc[0], o["ancestry"])
+    np.testing.assert_array_equal(hid[0], o["hidden"])
+
+
+def test_full_size_cfg2_properties(datasets_golden):
+    """BASELINE config 2 at full size (N=10,000, T=200): conservation, ancestor range, log-likelihood
+    agreement with the oracle (threaded C) and determinism of the run."""
+    Y = datasets_golden["cfg2_binom"]
+    a = dict(Y=Y, model="sir", theta=(0.25, 0.1), N=10000, npop=10000, mu=20)
+    eng, th = engine_for(a)
+    lz, st = eng.run(th[None], 0.1, 2024, 0)
+    assert st[0] == 0
+    hid, anc = eng.history(1)
+    assert np.all(hid[0].sum(axis=2) == 10000)
+    assert anc.min() >= 0 and anc.max() < 10000
+    o = oracle.particle_filter(Y, "sir", (0.25, 0.1), False, 0.1, 10000, 10000, 20, key=2024, filter_index=0)
+    np.testing.assert_array_equal(hid[0], o["hidden"])
+    np.testing.assert_array_equal(anc[0], o["ancestry"])
+    np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-8)
