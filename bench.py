@@ -160,6 +160,7 @@ def main():
         except (OSError, ValueError):
             traffic = None
     events_per_s = st["events"] / (st["step_ms"] / 1e3) if st["step_ms"] > 0 else None
+    lane_use = st["lane_iterations"] / st["wave_lane_slots"] if st["wave_lane_slots"] else None
 
     single = None
     if args.single_chain and rank == 0 and world == 1:
@@ -203,6 +204,7 @@ def main():
                          "kernel": "pf_step_kernel", "avg_launch_us": avg_launch_s * 1e6,
                          "bytes_per_particle_step": bytes_per_unit, "particle_steps_per_launch": units_per_launch},
             "events_per_s": events_per_s,
+            "ssa_lane_utilisation": lane_use,
             "resample_fallbacks": st["resample_fallbacks"],
             "gathered_draws_shape": list(gathered.shape),
             "cpu_baseline": base,

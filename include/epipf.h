@@ -73,6 +73,8 @@ typedef struct {
     int64_t particle_steps;      /* N x T_obs x chains that ran a filter */
     int64_t filters;             /* chain-filters run */
     int64_t resample_fallbacks;  /* draws resolved by the sequential bit-exact path */
+    int64_t lane_iterations;     /* SSA loop iterations summed over lanes (profiling on) */
+    int64_t wave_lane_slots;     /* SSA loop iterations x 64 summed over waves: lane_iterations / this = SIMD lane use */
 } epipf_stats;
 
 /* groups: G for the subgroup models (1 <= G <= 4), ignored (1) for SIR/SEIR.

@@ -278,7 +278,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     HIP_TRY(hipMemcpyAsync(c->h_status, c->status, sizeof(int32_t) * n_chains, hipMemcpyDeviceToHost, c->stream));
     if (log_zetas_out)
         HIP_TRY(hipMemcpyAsync(c->h_lz, c->log_zeta, sizeof(double) * (size_t)n_chains * c->T, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->h_counters, c->counters, sizeof(unsigned long long) * 2, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_counters, c->counters, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     memcpy(status_out, c->h_status, sizeof(int32_t) * n_chains);
     if (log_zetas_out) {
@@ -306,6 +306,8 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     }
     c->stats.events = (int64_t)c->h_counters[0];
     c->stats.resample_fallbacks = (int64_t)c->h_counters[1];
+    c->stats.lane_iterations = (int64_t)c->h_counters[2];
+    c->stats.wave_lane_slots = (int64_t)c->h_counters[3];
     c->stats.particle_steps += (int64_t)n_active * c->N * c->T;
     c->stats.filters += n_active;
     c->last_chains = n_chains;

@@ -28,10 +28,10 @@ __device__ __forceinline__ Block philox(uint32_t c0, uint32_t c1, uint32_t c2, u
                                         uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        const uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;   // one 32x32->64 multiply each
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }
     return Block{c0, c1, c2, c3};
@@ -53,13 +53,110 @@ struct ChainParam {
     uint32_t pad;
 };
 
+// ------------------------------------------------------------------------------- f64 log, table driven
+// log(x) for normal x > 0, within 1 ulp of glibc's correctly rounded log (exact near x = 1).  x = 2^k z with
+// z in [0.6875, 1.375) (glibc's OFF reduction); z is centred on one of 128 table points c_i
+// (LogTab: {1/c_i, log c_i}), r = z/c_i - 1 (|r| < 2^-8) and log1p(r) is a degree-7 polynomial.  Inputs within
+// 2^-8 of 1 bypass the table (r = x - 1 exactly).  ~20 instructions against ~45 for the library log.
+struct LogTab { double invc, logc; };
+constexpr int kLogTabEntries = 128;
+constexpr uint64_t kLogOff = 0x3FE6000000000000ull;   // 0.6875
+
+// one entry per thread (i < 128); the bin holding 1.0 gets exactly {1, 0}
+__device__ __forceinline__ void log_table_entry(LogTab* tab, int i) {
+    if (i < kLogTabEntries) {
+        const double c = __longlong_as_double((long long)(kLogOff + ((uint64_t)(2 * i + 1) << 44)));
+        const double ic = 1.0 / c;
+        const bool one = i == (int)(((0x3FF0000000000000ull - kLogOff) >> 45) & 127);
+        tab[i].invc = one ? 1.0 : ic;
+        tab[i].logc = one ? 0.0 : -log(ic);
+    }
+}
+
+__device__ __forceinline__ double fast_log(double x, const LogTab* __restrict__ tab) {
+    const uint64_t ix = (uint64_t)__double_as_longlong(x);
+    const uint64_t tmp = ix - kLogOff;
+    const int i = (int)((tmp >> 45) & 127);
+    const bool near1 = fabs(x - 1.0) < 0x1.0p-8;
+    const LogTab e = tab[i];
+    const int k = near1 ? 0 : (int)((int64_t)tmp >> 52);
+    const double z = near1 ? x : __longlong_as_double((long long)(ix - (tmp & (0xFFFull << 52))));
+    const double ic = near1 ? 1.0 : e.invc, lc = near1 ? 0.0 : e.logc;
+    const double r = fma(z, ic, -1.0);
+    const double kd = (double)k;
+    const double w = fma(kd, 0x1.62e42fefa3800p-1, lc);           // k*ln2_hi + log c (exact product)
+    const double hi = w + r;
+    double lo = (w - hi) + r;
+    lo = fma(kd, 0x1.ef35793c76730p-45, lo);                      // k*ln2_lo
+    double p = 1.0 / 7.0;
+    p = fma(r, p, -1.0 / 6.0);
+    p = fma(r, p, 1.0 / 5.0);
+    p = fma(r, p, -0.25);
+    p = fma(r, p, 1.0 / 3.0);
+    p = fma(r, p, -0.5);
+    return hi + fma(r * r, p, lo);                                // log1p(r) = r + r^2 P(r)
+}
+
+// 1/a to ~1 ulp: hardware reciprocal + two Newton steps
+__device__ __forceinline__ double recip(double a) {
+    double r = __builtin_amdgcn_rcp(a);
+    r = fma(fma(-a, r, 1.0), r, r);
+    return fma(fma(-a, r, 1.0), r, r);
+}
+
 // ------------------------------------------------------------------------------- Gillespie SSA
 // Direct method over [0, tmax] from state x (integers held in doubles, as the reference holds them),
 // gillespie_algo.py.  Event k of this lane draws Philox block (k, j, ptag, f): tau from (x,y), the
 // channel from (z,w).  Both uniforms are consumed before the overshoot test, as in the reference.
+//
+// Fast path + certified fallback: the channel decision of the reference is
+//   count_i [ fl(c_i / c_last) <= u ],  c = cumsum(fl(a_l / sum(a)))            (numpy choice, :63)
+// whose ratios agree with q_i = (a_0 + ... + a_i) * (1/sum a) to a few ulps.  When every q_i is farther than
+// kBand from u the decision is the reference's; otherwise the reference expression is evaluated exactly
+// (IEEE divisions in the reference's order).  The event time uses 1/sum(a) and log to ~1 ulp, so the
+// clock t can differ from the reference's by ulps; a step-boundary decision can then differ only when
+// t + tau lands within a few ulps of the step end (p ~ 1e-13 per particle-step).
+constexpr double kBand = 0x1.0p-44;
+
+__device__ __noinline__ bool sir_channel_exact(double beta, double gamma, double S, double I, double N, double u) {
+    const double a0 = ((beta * S) * I) / N, a1 = gamma * I;         // gillespie_algo.py:38-39
+    const double as = a0 + a1;
+    const double p0 = a0 / as, p1 = a1 / as;                       // :63
+    return (p0 / (p0 + p1)) <= u;
+}
+
+__device__ __noinline__ int seir_channel_exact(double beta, double alpha, double gamma, double S, double E, double I,
+                                               double N, double u) {
+    const double a0 = ((beta * S) * I) / N, a1 = alpha * E, a2 = gamma * I;   // :107-109
+    const double as = (a0 + a1) + a2;
+    const double p0 = a0 / as, p1 = a1 / as, p2 = a2 / as;
+    const double c1 = p0 + p1, c2 = c1 + p2;
+    return ((p0 / c2) <= u ? 1 : 0) + ((c1 / c2) <= u ? 1 : 0);       // :134
+}
+
+template <int G>
+__device__ __forceinline__ int subgroups_channel_exact(const double* th, const double* S, const double* I, double sumN,
+                                                       double u) {
+    constexpr int NCH = G * G + G;
+    const double gamma = th[G * G];
+    double a[NCH];
+    for (int g = 0; g < G; ++g) {                                      // :180-185
+        for (int g2 = 0; g2 < G; ++g2) a[g * (G + 1) + g2] = ((th[g * G + g2] * S[g2]) * I[g]) / sumN;
+        a[g * (G + 1) + G] = gamma * I[g];
+    }
+    double as = 0.0;
+    for (int i = 0; i < NCH; ++i) as = as + a[i];                      // :208
+    double cdf[NCH];
+    double run = 0.0;
+    for (int i = 0; i < NCH; ++i) { run = run + a[i] / as; cdf[i] = run; }
+    int ch = 0;
+    for (int i = 0; i < NCH - 1; ++i) ch += ((cdf[i] / cdf[NCH - 1]) <= u) ? 1 : 0;   // :209-212
+    return ch;
+}
+
 template <int MODEL, int G>
 __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
-                                             double tmax) {
+                                             double tmax, const LogTab* __restrict__ tab, int& iters) {
     double t = 0.0;
     uint32_t k = 0;
     int nev = 0;
@@ -67,15 +164,18 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
         const double beta = cp.theta[0], gamma = cp.theta[1];
         double S = x[0], I = x[1], R = x[2];
         const double N = (S + I) + R;                                  // gillespie_algo.py:35
+        const double invN = 1.0 / N;
         while (I > 0.0) {                                              // :48
             const Block r = philox(k, j, ptag, cp.f, cp.k0, cp.k1);
             ++k;
-            const double a0 = ((beta * S) * I) / N;                    // :38
-            const double a1 = gamma * I;                               // :39
-            const double as = a0 + a1;
-            const double tau = (1.0 / as) * (-log(1.0 - u01(r.x, r.y)));   // np.random.exponential, :62
-            const double p0 = a0 / as, p1 = a1 / as;                   // choice(p=a/sum(a)), :63
-            const bool second = (p0 / (p0 + p1)) <= u01(r.z, r.w);     // cdf/cdf[-1], searchsorted right
+            const double a0 = ((beta * S) * I) * invN;                 // :38
+            const double as = a0 + gamma * I;                          // :39
+            const double ri = recip(as);
+            const double tau = ri * (-fast_log(1.0 - u01(r.x, r.y), tab));   // np.random.exponential, :62
+            const double u = u01(r.z, r.w);
+            const double q = a0 * ri;
+            bool second = q <= u;                                      // choice(2, p=a/sum(a)), :63
+            if (fabs(q - u) <= kBand) second = sir_channel_exact(beta, gamma, S, I, N, u);
             if (t + tau > tmax) break;                                 // :65-66
             t = t + tau;
             if (second) { I -= 1.0; R += 1.0; } else { S -= 1.0; I += 1.0; }
@@ -86,16 +186,19 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
         const double beta = cp.theta[0], alpha = cp.theta[1], gamma = cp.theta[2];   // :92
         double S = x[0], E = x[1], I = x[2], R = x[3];
         const double N = ((S + E) + I) + R;                            // :104
+        const double invN = 1.0 / N;
         while (E > 0.0 || I > 0.0) {                                   // :119
             const Block r = philox(k, j, ptag, cp.f, cp.k0, cp.k1);
             ++k;
-            const double a0 = ((beta * S) * I) / N, a1 = alpha * E, a2 = gamma * I;
-            const double as = (a0 + a1) + a2;
-            const double tau = (1.0 / as) * (-log(1.0 - u01(r.x, r.y)));   // :133
-            const double p0 = a0 / as, p1 = a1 / as, p2 = a2 / as;
-            const double c1 = p0 + p1, c2 = c1 + p2;
+            const double a0 = ((beta * S) * I) * invN, a01 = a0 + alpha * E;
+            const double as = a01 + gamma * I;
+            const double ri = recip(as);
+            const double tau = ri * (-fast_log(1.0 - u01(r.x, r.y), tab));   // :133
             const double u = u01(r.z, r.w);
-            const int ch = ((p0 / c2) <= u ? 1 : 0) + ((c1 / c2) <= u ? 1 : 0);   // :134
+            const double q0 = a0 * ri, q1 = a01 * ri;
+            int ch = (q0 <= u ? 1 : 0) + (q1 <= u ? 1 : 0);            // :134
+            if (fabs(q0 - u) <= kBand || fabs(q1 - u) <= kBand)
+                ch = seir_channel_exact(beta, alpha, gamma, S, E, I, N, u);
             if (t + tau > tmax) break;                                 // :136-137
             t = t + tau;
             if (ch == 0) { S -= 1.0; E += 1.0; }
@@ -114,31 +217,37 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
             S[g] = x[3 * g]; I[g] = x[3 * g + 1]; R[g] = x[3 * g + 2];
             sumN = sumN + ((S[g] + I[g]) + R[g]);                      // sum(N), :176,:182
         }
+        const double invSumN = 1.0 / sumN;
         double infected = 0.0;
 #pragma unroll
         for (int g = 0; g < G; ++g) infected = infected + I[g];        // :192
         while (infected > 0.0) {                                       // :193
             const Block r = philox(k, j, ptag, cp.f, cp.k0, cp.k1);
             ++k;
-            double a[NCH];
+            double cum[NCH];
+            double run = 0.0;
 #pragma unroll
             for (int g = 0; g < G; ++g) {                              // channel order, :180-185
 #pragma unroll
-                for (int g2 = 0; g2 < G; ++g2) a[g * (G + 1) + g2] = ((cp.theta[g * G + g2] * S[g2]) * I[g]) / sumN;
-                a[g * (G + 1) + G] = gamma * I[g];
+                for (int g2 = 0; g2 < G; ++g2) {
+                    run = run + ((cp.theta[g * G + g2] * S[g2]) * I[g]) * invSumN;
+                    cum[g * (G + 1) + g2] = run;
+                }
+                run = run + gamma * I[g];
+                cum[g * (G + 1) + G] = run;
             }
-            double as = 0.0;
-#pragma unroll
-            for (int i = 0; i < NCH; ++i) as = as + a[i];              // sum(list(values)), :208
-            const double tau = (1.0 / as) * (-log(1.0 - u01(r.x, r.y)));
-            double cdf[NCH];
-            double run = 0.0;
-#pragma unroll
-            for (int i = 0; i < NCH; ++i) { run = run + a[i] / as; cdf[i] = run; }
+            const double ri = recip(run);
+            const double tau = ri * (-fast_log(1.0 - u01(r.x, r.y), tab));
             const double u = u01(r.z, r.w);
             int ch = 0;
+            bool close = false;
 #pragma unroll
-            for (int i = 0; i < NCH - 1; ++i) ch += ((cdf[i] / cdf[NCH - 1]) <= u) ? 1 : 0;   // :209-212
+            for (int i = 0; i < NCH - 1; ++i) {
+                const double q = cum[i] * ri;
+                ch += (q <= u) ? 1 : 0;
+                close |= fabs(q - u) <= kBand;
+            }
+            if (close) ch = subgroups_channel_exact<G>(cp.theta, S, I, sumN, u);
             if (t + tau > tmax) break;                                 // :215-216
             t = t + tau;
 #pragma unroll
@@ -156,6 +265,7 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
 #pragma unroll
         for (int g = 0; g < G; ++g) { x[3 * g] = S[g]; x[3 * g + 1] = I[g]; x[3 * g + 2] = R[g]; }
     }
+    iters = (int)k;
     return nev;
 }
 

@@ -91,13 +91,15 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
     using Sh = Shape<MODEL, G>;
     constexpr int C = Sh::C;
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    double* red = smem;                  // WG/64 (+pad)
-    double* bsum = smem + 16;            // B
-    double* bpex = bsum + a.B;           // B + WG
+    LogTab* tab = reinterpret_cast<LogTab*>(smem);       // 128 x 16 B log table (first: 16-B aligned)
+    double* red = smem + 2 * kLogTabEntries;             // WG/64 (+pad)
+    double* bsum = red + 16;                             // B
+    double* bpex = bsum + a.B;                           // B + WG
     const int chain = blockIdx.y;
     const int tid = threadIdx.x;
     const int j = blockIdx.x * WG + tid;
     if (a.status[chain] != 0) return;
+    for (int i = tid; i < kLogTabEntries; i += WG) log_table_entry(tab, i);   // published by the barriers below
     const ChainParam cp = a.cp[chain];
     const int prev = (p - 1) & 1, cur = p & 1;
     const size_t wprev = ((size_t)prev * a.max_chains + chain) * a.wstride;
@@ -117,7 +119,7 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
     if (blockIdx.x == 0 && tid == 0)
         a.log_zeta[(size_t)chain * a.T + p] = a.log_zeta[(size_t)chain * a.T + p - 1] + log(total / (double)a.N);
 
-    int nev = 0;
+    int nev = 0, iters = 0;
     double w = 0.0;
     if (j < a.N) {
         // (d) multinomial (or systematic) draw and certified search, pmcmc.py:188-190
@@ -141,17 +143,26 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
 #pragma unroll
         for (int c = 0; c < C; ++c) x[c] = (double)hp[c];
         const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
-        nev = ssa_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0);
+        nev = ssa_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, tab, iters);
         int32_t* hc = a.hidden + (size_t)chain * a.hist_stride + ((size_t)p * a.N + j) * C;
 #pragma unroll
         for (int c = 0; c < C; ++c) hc[c] = (int32_t)x[c];                        // :222-231
         // (a) weights of the new state against Y[p], used by step p+1, :178-181
         if (p + 1 < a.T) w = particle_weight<MODEL, G, OBS>(x, a.Y + (size_t)p * Sh::K, cp, a.lf, a.lf_max);
     }
-    if (a.count_events) {
-        unsigned long long e = (unsigned long long)nev;
-        for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
-        if ((tid & 63) == 0) atomicAdd(a.counters, e);
+    if (a.count_events) {  // accepted events; lane-iterations; wave-iterations x 64 (lane utilisation)
+        unsigned long long e = (unsigned long long)nev, li = (unsigned long long)iters;
+        int wmax = iters;
+        for (int o = 32; o > 0; o >>= 1) {
+            e += __shfl_xor(e, o, 64);
+            li += __shfl_xor(li, o, 64);
+            wmax = max(wmax, __shfl_xor(wmax, o, 64));
+        }
+        if ((tid & 63) == 0) {
+            atomicAdd(a.counters, e);
+            atomicAdd(a.counters + 2, li);
+            atomicAdd(a.counters + 3, 64ull * (unsigned long long)wmax);
+        }
     }
     if (p + 1 < a.T) {
         const double loc = block_inclusive_scan<WG>(w, red);
@@ -179,13 +190,16 @@ __global__ void path_sample_kernel(PathArgs a) {
 template <int MODEL, int G>
 __global__ __launch_bounds__(256) void simulate_kernel(SimArgs a) {
     constexpr int C = Shape<MODEL, G>::C;
+    __shared__ LogTab tab[kLogTabEntries];
+    if (threadIdx.x < kLogTabEntries) log_table_entry(tab, threadIdx.x);
+    __syncthreads();
     const int j = blockIdx.x * 256 + threadIdx.x;
-    int nev = 0;
+    int nev = 0, iters = 0;
     if (j < a.n) {
         double x[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) x[c] = (double)a.in[(size_t)j * C + c];
-        nev = ssa_propagate<MODEL, G>(x, *a.cp, (uint32_t)j, (a.step & 0xFFFFFFu) | kDomainSSA, a.tmax);
+        nev = ssa_propagate<MODEL, G>(x, *a.cp, (uint32_t)j, (a.step & 0xFFFFFFu) | kDomainSSA, a.tmax, tab, iters);
 #pragma unroll
         for (int c = 0; c < C; ++c) a.out[(size_t)j * C + c] = (int32_t)x[c];
     }
@@ -209,8 +223,8 @@ __global__ __launch_bounds__(WG) void resample_scan_kernel(ResampleArgs a) {
 template <int WG>
 __global__ __launch_bounds__(WG) void resample_search_kernel(ResampleArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    double* red = smem;
-    double* bsum = smem + 16;
+    double* red = smem + 2 * kLogTabEntries;
+    double* bsum = red + 16;
     double* bpex = bsum + a.B;
     const int j = blockIdx.x * WG + threadIdx.x;
     const double total = scan_block_sums<WG>(a.bsum, a.B, bpex, bsum, red);
@@ -227,7 +241,9 @@ __global__ __launch_bounds__(WG) void resample_search_kernel(ResampleArgs a) {
 }
 
 // ------------------------------------------------------------------------------- launchers
-size_t step_lds_bytes(int B, int wg) { return sizeof(double) * (size_t)(16 + B + B + wg); }
+size_t step_lds_bytes(int B, int wg) {
+    return sizeof(LogTab) * kLogTabEntries + sizeof(double) * (size_t)(16 + B + B + wg);
+}
 
 template <int MODEL, int G, int OBS, int WG>
 static hipError_t launch_filter_t(const StepArgs& a, int n_chains, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,

@@ -34,6 +34,8 @@ class Stats(ctypes.Structure):
         ("particle_steps", ctypes.c_int64),
         ("filters", ctypes.c_int64),
         ("resample_fallbacks", ctypes.c_int64),
+        ("lane_iterations", ctypes.c_int64),
+        ("wave_lane_slots", ctypes.c_int64),
     ]
 
     def as_dict(self):

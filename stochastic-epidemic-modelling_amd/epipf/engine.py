@@ -18,6 +18,8 @@ MODEL_IDS = {"sir": _lib.SIR, "seir": _lib.SEIR, "sir_subgroups": _lib.SIR_SUBGR
 def model_id(type_model):
     """Accept this package's ModelType, the reference's ModelType (same .value strings) or a string."""
     name = getattr(type_model, "value", type_model)
+    if isinstance(name, (int, np.integer)) and 0 <= int(name) <= 3:
+        return int(name)
     if isinstance(name, str) and name.lower() in MODEL_IDS:
         return MODEL_IDS[name.lower()]
     raise ValueError(f"unknown model type {type_model!r}")

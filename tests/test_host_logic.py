@@ -1,0 +1,120 @@
+"""Host-side MH logic (epipf.pmcmc) on CPU: the GPU engine is replaced, inside this test only, by a
+stand-in that answers from the oracle, so the accept/reject / RNG-order / probs=None / subgroup /
+adaptive logic is checked against the reference's own PMCMC runs (tests/golden/pmcmc_golden.npz)
+without a GPU.  The product has no such fallback: epipf.engine.Engine always requires libepipf + a GPU."""
+import numpy as np
+import pytest
+
+import oracle
+from epipf import pmcmc as pm
+from epipf.engine import model_id, n_compartments
+
+
+class OracleEngine:
+    """Test double with Engine's interface (set_observations / set_population / run / path_sample)."""
+
+    def __init__(self, mid, G, N, T, chains):
+        self.mid, self.G, self.N, self.t_max, self.max_chains = mid, G, N, T, chains
+        self.C = n_compartments(mid, G)
+        self.hist = {}
+
+    def set_observations(self, Y):
+        self.Y = np.asarray(Y, dtype=float)
+        self.T = self.Y.shape[0]
+
+    def set_population(self, npop, mu):
+        self.npop, self.mu = np.atleast_1d(npop), np.atleast_1d(mu)
+
+    def run(self, thetas, probs, keys, fidx, observations=False, active=None, resample="multinomial"):
+        n = len(thetas)
+        probs = np.broadcast_to(probs, (n,))
+        keys = np.broadcast_to(np.asarray(keys, dtype=np.uint64), (n,))
+        fidx = np.broadcast_to(fidx, (n,))
+        lz = np.zeros((n, self.T))
+        st = np.zeros(n, dtype=np.int32)
+        name = ["sir", "seir", "sir_subgroups", "sir_subgroups2"][self.mid]
+        for c in range(n):
+            if active is not None and not active[c]:
+                st[c] = 2
+                continue
+            th = thetas[c]
+            if self.mid >= 2:
+                th = (th[:self.G * self.G].reshape(self.G, self.G), th[-1])
+            npop = self.npop if self.mid >= 2 else float(self.npop[0])
+            mu = self.mu if self.mid >= 2 else float(self.mu[0])
+            o = oracle.particle_filter(self.Y, name, th, observations, float(probs[c]), self.N, npop, mu,
+                                       key=int(keys[c]), filter_index=int(fidx[c]), resample=resample)
+            st[c] = o["status"]
+            lz[c] = o["log_zetas"]
+            self.hist[c] = (o["hidden"], o["ancestry"])
+        return lz, st
+
+    def path_sample(self, chosen):
+        out = np.zeros((len(chosen), self.T, self.C), dtype=np.int32)
+        for c, ch in enumerate(chosen):
+            if c not in self.hist:
+                continue
+            hid, anc = self.hist[c]
+            out[c, -1] = hid[-1, ch]
+            for p in range(self.T - 2, -1, -1):
+                ch = anc[p, ch]
+                out[c, p] = hid[p, ch]
+        return out
+
+
+@pytest.fixture
+def oracle_engine(monkeypatch):
+    def fake_get_engine(type_model, groups, n_particles, T, chains=1, device=0):
+        mid = model_id(type_model)
+        return OracleEngine(mid, groups if mid >= 2 else 1, int(n_particles), T, chains)
+    monkeypatch.setattr(pm, "get_engine", fake_get_engine)
+
+
+@pytest.mark.parametrize("name", ["sir_small", "sir_p", "sub"])
+def test_mh_loop_reproduces_reference_trace(oracle_engine, pmcmc_golden, name):
+    rec = pmcmc_golden["pmcmc_" + name]
+    model = str(rec["model"])
+    sub = model.startswith("SIR_SUB")
+    sigma = None if rec["sigma"].size == 0 else rec["sigma"]
+    probs = None if float(rec["probs"]) < 0 else float(rec["probs"])
+    pm.seed_stream(int(rec["key"]), 0)
+    np.random.seed(int(rec["seed"]))
+    th, lk, tr = pm.particle_mcmc(rec["Y"], model.lower(), list(rec["params"]), float(rec["h"]),
+                                  adaptive=bool(rec["adaptive"]), sigma=sigma, n_chains=int(rec["iters"]),
+                                  probs=probs, n_particles=int(rec["N"]),
+                                  n_population=rec["npop"] if sub else float(rec["npop"][0]),
+                                  mu=rec["mu"] if sub else float(rec["mu"][0]), progress=False)
+    np.testing.assert_array_equal(th, rec["thetas"])
+    np.testing.assert_array_equal(tr, rec["trajs"])
+    np.testing.assert_allclose(lk, rec["likelihoods"], rtol=1e-9)
+    assert pm._STREAM.next_filter == int(rec["n_filters"])
+
+
+def test_log_ratio_matches_reference_ratio_when_finite():
+    from scipy.stats import multivariate_normal  # noqa: F401
+    rs = np.random.RandomState(0)
+    for _ in range(200):
+        lz_new, lz_old = rs.uniform(-60, -10, 2)
+        th_new, th_old = rs.uniform(0.5, 2, 2), rs.uniform(0.5, 2, 2)
+        ref = pm._reference_ratio(np.exp(lz_new), np.exp(lz_old), th_new, th_old, [2.0, 1.0], 0.01 * np.eye(2))
+        assert abs(pm._log_ratio(lz_new, lz_old) - ref) <= 1e-9 * max(1.0, ref)
+
+
+def test_log_ratio_survives_underflow():
+    # zetas underflow at T~200 (pmcmc.py:183): the reference's ratio is 0/0 -> nan -> min(1, nan) = 1
+    assert pm._reference_ratio(np.float64(0.0), np.float64(0.0), np.ones(2), np.ones(2), [1.0, 1.0],
+                               np.eye(2)) == 1
+    assert pm._log_ratio(-900.0, -905.0) == 1.0
+    assert abs(pm._log_ratio(-905.0, -900.0) - np.exp(-5.0)) < 1e-15
+
+
+def test_multichain_lockstep_equals_independent_runs(oracle_engine, datasets_golden):
+    Y = datasets_golden["cfg1_binom"][:8]
+    kw = dict(Y=Y, type_model="sir", parameters=[2.0, 1.0], h=0.02, n_chains=6, probs=0.1, n_particles=16,
+              n_population=200, mu=20, mh_ratio="log")
+    multi = pm.particle_mcmc_chains(**kw, chains=3, seed=5)
+    for c in range(3):
+        single = pm.particle_mcmc_chains(**kw, rngs=[np.random.RandomState(5 + c)], keys=[pm.chain_key(5, c)])[0]
+        np.testing.assert_array_equal(single.thetas, multi[c].thetas)
+        np.testing.assert_array_equal(single.sampled_trajs, multi[c].sampled_trajs)
+        np.testing.assert_allclose(single.log_likelihoods, multi[c].log_likelihoods)
