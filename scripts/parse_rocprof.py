@@ -1,0 +1,55 @@
+"""Summarise a scripts/profile.sh session: per-kernel stats of the trace pass and per-launch PMC averages
+of pf_step_kernel.  Writes <dir>/pmc_step_kernel.json (copied to profiles/ when committed; bench.py reads
+profiles/pmc_step_kernel.json for roofline.traffic).
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE
+counts 64 B per 128-B request of a wide coalesced stream (read side up to 2x low).  We report the raw
+sum and the read-doubled upper estimate; `hbm_bytes_per_launch` is the raw sum (uncorrected, stated)."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def rows(path):
+    with open(path, newline="") as f:
+        return list(csv.DictReader(f))
+
+
+def main(d):
+    out = {}
+    for p in glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True):
+        print(f"# kernel stats: {p}")
+        for r in rows(p):
+            print(f"  {r['Name'][:90]:90s} calls={r['Calls']:>6s} avg_us={float(r['AverageNs'])/1e3:10.2f} "
+                  f"total_ms={float(r['TotalDurationNs'])/1e6:9.2f} pct={float(r['Percentage']):6.2f}")
+            if "pf_step_kernel" in r["Name"]:
+                out["trace_avg_us"] = float(r["AverageNs"]) / 1e3
+                out["trace_calls"] = int(r["Calls"])
+                out["kernel"] = r["Name"]
+    per = defaultdict(lambda: defaultdict(float))   # counter -> dispatch -> value
+    meta = {}
+    for p in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
+        for r in rows(p):
+            if "pf_step_kernel" not in r["Kernel_Name"]:
+                continue
+            per[r["Counter_Name"]][(p, r["Dispatch_Id"])] += float(r["Counter_Value"])
+            meta = {k: r.get(k) for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "VGPR_Count",
+                                          "SGPR_Count", "Scratch_Size")}
+    avg = {k: sum(v.values()) / len(v) for k, v in per.items() if v}
+    out["pmc_avg_per_launch"] = avg
+    out["pmc_launches"] = {k: len(v) for k, v in per.items()}
+    out["dispatch"] = meta
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        raw = (avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024.0
+        out["hbm_bytes_per_launch"] = raw
+        out["hbm_bytes_per_launch_read_doubled"] = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024.0
+    print(json.dumps(out, indent=1))
+    with open(os.path.join(d, "pmc_step_kernel.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
