@@ -92,13 +92,14 @@ def main():
     import torch
 
     from epipf import datasets
+    from epipf.distributed import gather_draws, pack_draws, shard
     from epipf.pmcmc import ChainSampler, chain_key
 
     Y, meta = datasets.benchmark_dataset(args.config)
     N, T = args.particles, Y.shape[0]
     C = args.chains
-    gid = [rank * C + c for c in range(C)]
-    sampler = ChainSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=args.warmup + args.steps + 1,
+    gid = shard(C * world, world, rank)                              # global chain ids of this rank
+    sampler = ChainSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=args.warmup + args.steps + 2,
                            observations=meta.get("observations", False), probs=meta["probs"], n_particles=N,
                            n_population=meta["n_population"], mu=meta["mu"],
                            rngs=[np.random.RandomState(args.seed + g) for g in gid],
@@ -113,27 +114,25 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    from epipf import _lib
     eng.reset_stats()
-    eng.set_profiling(True)
+    eng.set_profiling(_lib.PROFILE_TIMING)       # HIP events only: the timed kernels are the production ones
     barrier()
     t0 = time.perf_counter()
     filters = 0
     for _ in range(args.steps):
         filters += sampler.step()
-    # end of run: gather the posterior draws of every rank's chains over RCCL (xGMI)
-    draws = np.concatenate([sampler.thetas[:, :sampler.i].reshape(C, -1),
-                            sampler.loglik[:, :sampler.i]], axis=1)
-    if dist is not None:
-        local_t = torch.from_numpy(draws).to(f"cuda:{local}")
-        out = [torch.empty_like(local_t) for _ in range(world)]
-        dist.all_gather(out, local_t)
-        gathered = torch.cat(out).cpu().numpy()
-    else:
-        gathered = draws
+    # end of run: gather every rank's posterior draws over RCCL (xGMI), SURVEY.md §8e
+    gathered = gather_draws(pack_draws(sampler.results(), upto=sampler.i), local)
     barrier()
     dt = time.perf_counter() - t0
-    eng.set_profiling(False)
     st = eng.stats()
+    # one extra, untimed MH iteration with device counters on: SSA events/s and SIMD lane use
+    eng.reset_stats()
+    eng.set_profiling(_lib.PROFILE_COUNTERS)
+    sampler.step()
+    eng.set_profiling(_lib.PROFILE_OFF)
+    cst = eng.stats()
 
     # max over ranks of the wall time; sum of filters
     if dist is not None:
@@ -159,8 +158,8 @@ def main():
             traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
-    events_per_s = st["events"] / (st["step_ms"] / 1e3) if st["step_ms"] > 0 else None
-    lane_use = st["lane_iterations"] / st["wave_lane_slots"] if st["wave_lane_slots"] else None
+    events_per_s = cst["events"] / (cst["step_ms"] / 1e3) if cst["step_ms"] > 0 else None
+    lane_use = cst["lane_iterations"] / cst["wave_lane_slots"] if cst["wave_lane_slots"] else None
 
     single = None
     if args.single_chain and rank == 0 and world == 1:
@@ -206,6 +205,7 @@ def main():
             "events_per_s": events_per_s,
             "ssa_lane_utilisation": lane_use,
             "resample_fallbacks": st["resample_fallbacks"],
+            "events_per_particle_step": cst["events"] / cst["particle_steps"] if cst["particle_steps"] else None,
             "gathered_draws_shape": list(gathered.shape),
             "cpu_baseline": base,
         }

@@ -119,7 +119,12 @@ int epipf_simulate(epipf_ctx* ctx, int n, const int32_t* states_in, const double
 int epipf_resample(epipf_ctx* ctx, int n, const double* w, const double* u, int32_t* out,
                    int64_t* fallbacks_out);
 
-int epipf_set_profiling(epipf_ctx* ctx, int enable);
+/* Profiling levels: OFF; TIMING = HIP events around the init / step kernels (step_ms, init_ms), no effect on
+ * the kernels; COUNTERS = TIMING + device counters of SSA events and lane use (a few atomics per wave). */
+#define EPIPF_PROFILE_OFF 0
+#define EPIPF_PROFILE_TIMING 1
+#define EPIPF_PROFILE_COUNTERS 2
+int epipf_set_profiling(epipf_ctx* ctx, int level);
 int epipf_get_stats(epipf_ctx* ctx, epipf_stats* out);
 int epipf_reset_stats(epipf_ctx* ctx);
 

@@ -74,7 +74,8 @@ struct epipf_ctx {
     double* h_lz = nullptr;
     unsigned long long* h_counters = nullptr;
     int T = 0, lf_max = -1, lf_cap = 0, last_chains = 0, last_T = 0;
-    bool have_Y = false, have_pop = false, have_run = false, profiling = false;
+    bool have_Y = false, have_pop = false, have_run = false;
+    int profiling = 0;   // EPIPF_PROFILE_* level
     double npop[kMaxG] = {0}, mu[kMaxG] = {0}, emu[kMaxG] = {0};
     int kmax[kMaxG] = {0};
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -158,18 +159,18 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     rc |= dalloc(&c->bsum, 2 * (size_t)max_chains * c->bstride);
     rc |= dalloc(&c->log_zeta, (size_t)max_chains * t_max);
     rc |= dalloc(&c->cp, (size_t)max_chains);
-    rc |= dalloc(&c->counters, 4);
+    rc |= dalloc(&c->counters, (size_t)kCounterSlots * kCounterStride);
     if (rc) { free_ctx(c); return EPIPF_ENOMEM; }
     if (hipHostMalloc((void**)&c->h_cp, sizeof(ChainParam) * max_chains) != hipSuccess ||
         hipHostMalloc((void**)&c->h_status, sizeof(int32_t) * max_chains) != hipSuccess ||
         hipHostMalloc((void**)&c->h_lz, sizeof(double) * (size_t)max_chains * t_max) != hipSuccess ||
-        hipHostMalloc((void**)&c->h_counters, sizeof(unsigned long long) * 4) != hipSuccess) {
+        hipHostMalloc((void**)&c->h_counters, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride) != hipSuccess) {
         free_ctx(c);
         return fail(EPIPF_ENOMEM, "hipHostMalloc failed");
     }
     for (auto& e : c->ev)
         if (hipEventCreate(&e) != hipSuccess) { free_ctx(c); return fail(EPIPF_EHIP, "hipEventCreate failed"); }
-    if (hipMemsetAsync(c->counters, 0, 4 * sizeof(unsigned long long), c->stream) != hipSuccess ||
+    if (hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
         free_ctx(c);
         return fail(EPIPF_EHIP, "counter init failed");
@@ -263,7 +264,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
 
     StepArgs a{};
     a.N = c->N; a.T = c->T; a.B = c->B; a.wg = c->wg; a.max_chains = c->max_chains;
-    a.resample_mode = resample_mode; a.count_events = c->profiling ? 1 : 0; a.lf_max = c->lf_max;
+    a.resample_mode = resample_mode; a.count_events = c->profiling >= EPIPF_PROFILE_COUNTERS ? 1 : 0; a.lf_max = c->lf_max;
     a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride; a.wstride = c->wstride; a.bstride = c->bstride;
     a.delta = (8.0 * (double)c->N + 256.0) * 0x1.0p-53;
     a.Y = c->Y; a.lf = c->lf; a.cp = c->cp; a.hidden = c->hidden; a.ancestry = c->ancestry;
@@ -278,7 +279,8 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     HIP_TRY(hipMemcpyAsync(c->h_status, c->status, sizeof(int32_t) * n_chains, hipMemcpyDeviceToHost, c->stream));
     if (log_zetas_out)
         HIP_TRY(hipMemcpyAsync(c->h_lz, c->log_zeta, sizeof(double) * (size_t)n_chains * c->T, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->h_counters, c->counters, sizeof(unsigned long long) * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_counters, c->counters, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride, hipMemcpyDeviceToHost,
+                           c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     memcpy(status_out, c->h_status, sizeof(int32_t) * n_chains);
     if (log_zetas_out) {
@@ -304,10 +306,13 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
         c->stats.step_ms += ms_step;
         c->stats.step_launches += c->T - 1;
     }
-    c->stats.events = (int64_t)c->h_counters[0];
-    c->stats.resample_fallbacks = (int64_t)c->h_counters[1];
-    c->stats.lane_iterations = (int64_t)c->h_counters[2];
-    c->stats.wave_lane_slots = (int64_t)c->h_counters[3];
+    unsigned long long tot[kNumCounters] = {0, 0, 0, 0};
+    for (int sl = 0; sl < kCounterSlots; ++sl)
+        for (int k = 0; k < kNumCounters; ++k) tot[k] += c->h_counters[(size_t)sl * kCounterStride + k];
+    c->stats.events = (int64_t)tot[0];
+    c->stats.resample_fallbacks = (int64_t)tot[1];
+    c->stats.lane_iterations = (int64_t)tot[2];
+    c->stats.wave_lane_slots = (int64_t)tot[3];
     c->stats.particle_steps += (int64_t)n_active * c->N * c->T;
     c->stats.filters += n_active;
     c->last_chains = n_chains;
@@ -440,7 +445,8 @@ int epipf_resample(epipf_ctx* c, int n, const double* w, const double* u, int32_
 
 int epipf_set_profiling(epipf_ctx* c, int enable) {
     if (!c) return fail(EPIPF_EINVAL, "NULL context");
-    c->profiling = enable != 0;
+    if (enable < EPIPF_PROFILE_OFF || enable > EPIPF_PROFILE_COUNTERS) return fail(EPIPF_EINVAL, "bad profiling level %d", enable);
+    c->profiling = enable;
     return EPIPF_OK;
 }
 
@@ -453,7 +459,7 @@ int epipf_get_stats(epipf_ctx* c, epipf_stats* out) {
 int epipf_reset_stats(epipf_ctx* c) {
     if (!c) return fail(EPIPF_EINVAL, "NULL context");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipMemsetAsync(c->counters, 0, 4 * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     memset(&c->stats, 0, sizeof c->stats);
     return EPIPF_OK;

@@ -7,6 +7,16 @@
 
 namespace epipf {
 
+// Device counters are spread over kCounterSlots cache lines: same-address atomics from every wave serialise
+// (~10 ns each on MI355X), which at 5k waves per launch cost more than the launch itself.
+constexpr int kCounterSlots = 64;
+constexpr int kCounterStride = 16;   // u64 per slot = 128 B
+constexpr int kNumCounters = 4;
+
+__device__ __forceinline__ unsigned long long* counter_slot(unsigned long long* base) {
+    return base + (size_t)((blockIdx.x + 7u * blockIdx.y) & (kCounterSlots - 1)) * kCounterStride;
+}
+
 // HBM layout (per context, sized at create for max_chains x t_max x n_particles):
 //   hidden   int32 [max_chains][t_max][N][C]      particle states (the reference's hidden_process)
 //   ancestry int32 [max_chains][t_max][N]         resampled parent indices (row 0 zeros)
@@ -29,7 +39,8 @@ struct StepArgs {
     double* bsum;
     double* log_zeta;
     int32_t* status;
-    unsigned long long* counters;  // [0] events, [1] resample fallbacks
+    unsigned long long* counters;  // [kCounterSlots][kCounterStride]: [0] events, [1] resample fallbacks,
+                                   // [2] SSA lane-iterations, [3] wave-iterations x 64 (summed on the host)
     double npop[kMaxG], mu[kMaxG], emu[kMaxG];
     int kmax[kMaxG];
 };

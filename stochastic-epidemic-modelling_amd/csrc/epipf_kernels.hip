@@ -135,7 +135,7 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
         bool fb;
         int anc = resample_search<WG>(U, bpex, bsum, a.B, total, a.wloc + wprev, a.wraw + wprev, a.N, a.delta, fb);
         anc = min(max(anc, 0), a.N - 1);
-        if (fb) atomicAdd(a.counters + 1, 1ull);
+        if (fb) atomicAdd(counter_slot(a.counters) + 1, 1ull);
         a.ancestry[(size_t)chain * a.anc_stride + (size_t)p * a.N + j] = anc;   // :193
         // (f) gather the parent state, (g) propagate over [0, 1], :195-220
         const int32_t* hp = a.hidden + (size_t)chain * a.hist_stride + ((size_t)(p - 1) * a.N + anc) * C;
@@ -159,9 +159,10 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
             wmax = max(wmax, __shfl_xor(wmax, o, 64));
         }
         if ((tid & 63) == 0) {
-            atomicAdd(a.counters, e);
-            atomicAdd(a.counters + 2, li);
-            atomicAdd(a.counters + 3, 64ull * (unsigned long long)wmax);
+            unsigned long long* slot = counter_slot(a.counters);
+            atomicAdd(slot, e);
+            atomicAdd(slot + 2, li);
+            atomicAdd(slot + 3, 64ull * (unsigned long long)wmax);
         }
     }
     if (p + 1 < a.T) {

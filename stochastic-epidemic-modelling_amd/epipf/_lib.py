@@ -15,6 +15,7 @@ STATUS_OK, STATUS_DEGENERATE, STATUS_SKIPPED = 0, 1, 2
 SIR, SEIR, SIR_SUBGROUPS, SIR_SUBGROUPS2 = 0, 1, 2, 3
 OBS_BINOMIAL, OBS_NORMAL = 0, 1
 RESAMPLE_MULTINOMIAL, RESAMPLE_SYSTEMATIC = 0, 1
+PROFILE_OFF, PROFILE_TIMING, PROFILE_COUNTERS = 0, 1, 2
 ABI_VERSION = 1
 
 EXPORTS = (

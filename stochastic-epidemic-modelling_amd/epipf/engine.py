@@ -153,8 +153,14 @@ class Engine:
         return (None if rc == _lib.STATUS_DEGENERATE else out), int(fb[0])
 
     # ------------------------------------------------------------------ stats
-    def set_profiling(self, on=True):
-        check(self._L.epipf_set_profiling(self._h, 1 if on else 0), "epipf_set_profiling")
+    def set_profiling(self, level=_lib.PROFILE_COUNTERS):
+        """level: PROFILE_OFF / PROFILE_TIMING (HIP events only, kernels unchanged) / PROFILE_COUNTERS
+        (also device counters of SSA events and lane use).  True/False map to COUNTERS/OFF."""
+        if level is True:
+            level = _lib.PROFILE_COUNTERS
+        elif level is False or level is None:
+            level = _lib.PROFILE_OFF
+        check(self._L.epipf_set_profiling(self._h, int(level)), "epipf_set_profiling")
 
     def stats(self):
         s = _lib.Stats()

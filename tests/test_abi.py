@@ -61,3 +61,5 @@ def test_constants_match_header():
     assert int(defs["EPIPF_SIR_SUBGROUPS2"]) == _lib.SIR_SUBGROUPS2
     assert int(defs["EPIPF_RESAMPLE_SYSTEMATIC"]) == _lib.RESAMPLE_SYSTEMATIC
     assert int(defs["EPIPF_ABI_VERSION"]) == _lib.ABI_VERSION
+    assert int(defs["EPIPF_PROFILE_TIMING"]) == _lib.PROFILE_TIMING
+    assert int(defs["EPIPF_PROFILE_COUNTERS"]) == _lib.PROFILE_COUNTERS
