@@ -29,6 +29,14 @@ def main(d):
                 out["trace_avg_us"] = float(r["AverageNs"]) / 1e3
                 out["trace_calls"] = int(r["Calls"])
                 out["kernel"] = r["Name"]
+    for p in glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursive=True):
+        ks = sorted((r for r in rows(p) if "pf_step_kernel" in r["Kernel_Name"]), key=lambda r: int(r["Start_Timestamp"]))
+        durs = sorted((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in ks)
+        if durs:
+            n = len(durs)
+            print(f"# pf_step_kernel durations (us) over {n} launches: min {durs[0]:.1f} p50 {durs[n // 2]:.1f} "
+                  f"p90 {durs[int(n * .9)]:.1f} p99 {durs[int(n * .99)]:.1f} max {durs[-1]:.1f} "
+                  f"sum {sum(durs) / 1e3:.1f} ms; launches > 5x median: {sum(x > 5 * durs[n // 2] for x in durs)}")
     per = defaultdict(lambda: defaultdict(float))   # counter -> dispatch -> value
     meta = {}
     for p in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):

@@ -85,6 +85,15 @@ struct epipf_ctx {
     void* scratch = nullptr;
 };
 
+// K = N + 2D + 8 of the resampling certificate (epipf_device.hpp): D bounds the depth of the parallel
+// reduction tree behind every prefix: in-block scan (6 shuffle levels + <=4 wave offsets + 1) = 11 <= 16,
+// block-sum scan 16 + 2 * ceil(B / WG) sequential chunk adds, +2 for the final adds.
+static double cert_k(int N, int B, int wg) {
+    const int per = (B + wg - 1) / wg;
+    const int D = 34 + 2 * per;
+    return (double)N + 2.0 * D + 8.0;
+}
+
 static int theta_dim(int model, int G) { return model == EPIPF_SIR ? 2 : model == EPIPF_SEIR ? 3 : G * G + 1; }
 
 static void free_ctx(epipf_ctx* c) {
@@ -266,7 +275,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     a.N = c->N; a.T = c->T; a.B = c->B; a.wg = c->wg; a.max_chains = c->max_chains;
     a.resample_mode = resample_mode; a.count_events = c->profiling >= EPIPF_PROFILE_COUNTERS ? 1 : 0; a.lf_max = c->lf_max;
     a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride; a.wstride = c->wstride; a.bstride = c->bstride;
-    a.delta = (8.0 * (double)c->N + 256.0) * 0x1.0p-53;
+    a.cert_k = cert_k(c->N, c->B, c->wg);
     a.Y = c->Y; a.lf = c->lf; a.cp = c->cp; a.hidden = c->hidden; a.ancestry = c->ancestry;
     a.wraw = c->wraw; a.wloc = c->wloc; a.bsum = c->bsum; a.log_zeta = c->log_zeta; a.status = c->status;
     a.counters = c->counters;
@@ -418,7 +427,7 @@ int epipf_resample(epipf_ctx* c, int n, const double* w, const double* u, int32_
     if (ensure_scratch(c, need)) return EPIPF_ENOMEM;
     char* p = (char*)c->scratch;
     ResampleArgs a{};
-    a.N = n; a.B = B; a.delta = (8.0 * (double)n + 256.0) * 0x1.0p-53;
+    a.N = n; a.B = B; a.cert_k = cert_k(n, B, 256);
     double* dw = (double*)p; p += nw;
     double* du = (double*)p; p += nw;
     a.wraw = (double*)p; p += nw;

@@ -347,32 +347,27 @@ __device__ __forceinline__ double block_inclusive_scan(double x, double* lds) {
 }
 
 // ------------------------------------------------------------------------------- resampling
-// numpy legacy choice(range(N), N, p=w/sum(w)) for ONE uniform U, exactly (pmcmc.py:185-190):
-//   S = sum(w) (sequential), q = w/S, c = cumsum(q) (sequential), a = #{i : c_i / c_{N-1} <= U}.
-// Used only when the fast parallel search below cannot certify its answer.
-__device__ __noinline__ int resample_exact(double U, const double* w, int N) {
-    double S = 0.0;
-    for (int i = 0; i < N; ++i) S = S + w[i];
-    double c = 0.0;
-    for (int i = 0; i < N; ++i) c = c + w[i] / S;
-    const double last = c;
-    c = 0.0;
-    for (int i = 0; i < N; ++i) {
-        c = c + w[i] / S;
-        if (c / last > U) return i;
-    }
-    return N - 1;
+// numpy legacy choice(range(N), N, p=w/sum(w)) for uniform U (pmcmc.py:185-190) is
+//   S = sum(w) (Python builtin: sequential), q = w/S, c = cumsum(q) (sequential), cdf = c / c[N-1],
+//   a = searchsorted(cdf, U, 'right') = first i with cdf_i > U.
+// The device searches a parallel CDF v_i = (block prefix + in-block prefix) / total instead and certifies
+// the answer against the reference's: with r_i = W_i / W the exact ratio of prefix sums,
+//   |cdf_i / r_i - 1| <= (i + N + 2) u      (sequential sum, quotients, cumsum, final division)
+//   |v_i / r_i - 1|   <= (2D + 1) u         (D = depth of the parallel reduction tree)
+// so |cdf_i - v_i| <= delta_i = (i + K) u v_i (1 + 2^-20), K = N + 2D + 8, u = 2^-53.
+// v_{a-1} + delta_{a-1} < U < v_a - delta_a proves cdf_{a-1} <= U < cdf_a, i.e. a is numpy's answer.
+// Draws that fail the test are resolved exactly by resample_exact_wave.
+__device__ __forceinline__ double cert_halfwidth(int i, double v, double cert_k) {
+    return ((double)i + cert_k) * 0x1.00001p-53 * v;
 }
 
-// Two-level search of the parallel CDF v_j = (bpex[b] + wloc[j]) / total (bpex: exclusive prefix of the
-// block sums, in LDS; wloc: in-block inclusive prefix, in HBM/L2).  The answer is certified against
-// the reference's sequential CDF: if v_{a-1} < U - delta and v_a > U + delta, every CDF within delta of
-// v (the sequential one included: delta bounds both roundings) puts U in slot a.
-// Otherwise the draw falls back to resample_exact.
+// Two-level search of v (bpex: exclusive prefix of the block sums and bsum: block sums, both in LDS;
+// wloc: in-block inclusive prefix, in HBM/L2).  Returns the candidate index; `certified` says whether the
+// bracket test above proved it.
 template <int WG>
 __device__ __forceinline__ int resample_search(double U, const double* bpex, const double* bsum, int B,
-                                               double total, const double* wloc, const double* wraw, int N,
-                                               double delta, bool& fell_back) {
+                                               double total, const double* wloc, int N, double cert_k,
+                                               bool& certified) {
     int lo = 0, hi = B - 1;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
@@ -386,16 +381,78 @@ __device__ __forceinline__ int resample_search(double U, const double* bpex, con
         const int m = (l + h) >> 1;
         if ((base + L[m]) / total > U) h = m; else l = m + 1;
     }
+    const int a = b * WG + l;
     const double va = (base + L[l]) / total;
     const double vp = (l > 0) ? (base + L[l - 1]) / total
                               : (b > 0 ? (bpex[b - 1] + bsum[b - 1]) / total : -1.0);
-    int a = b * WG + l;
-    fell_back = false;
-    if (!(va > U + delta) || !(vp < U - delta) || a >= N) {
-        fell_back = true;
-        a = resample_exact(U, wraw, N);
-    }
+    certified = (va - cert_halfwidth(a, va, cert_k) > U) &&
+                (a == 0 || vp + cert_halfwidth(a - 1, vp, cert_k) < U) && a < N;
     return a;
+}
+
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __hiloint2double(hi, lo);
+}
+
+// The exact reference draw for every lane of the wave with need == true, all 64 lanes cooperating (call
+// from wave-uniform control flow; every lane must be active).  The weights are streamed in coalesced chunks
+// of 64; the sequential sums run on values broadcast with v_readlane, in the reference's order:
+//   pass 1  S = (((w_0 + w_1) + w_2) + ...)
+//   pass 2  last = c_{N-1},  c_i = c_{i-1} + w_i / S
+//   pass 3  first i with fl(c_i / last) > U, per needing lane (c_i / last via a certified product, with
+//           the IEEE division only within a few ulps of U); stops once every needing lane is resolved.
+// Cost ~3 x N dependent f64 adds for the wave (~0.1 ms at N = 10^4) instead of 3N dependent HBM loads.
+__device__ __noinline__ int resample_exact_wave(bool need, double U, const double* __restrict__ w, int N) {
+    const int lane = threadIdx.x & 63;
+    double S = 0.0;
+    double x = (lane < N) ? w[lane] : 0.0;
+    for (int base = 0; base < N; base += 64) {
+        const double xn = (base + 64 + lane < N) ? w[base + 64 + lane] : 0.0;   // prefetch the next chunk
+        if (base + 64 <= N) {
+#pragma unroll
+            for (int l = 0; l < 64; ++l) S = S + readlane_f64(x, l);
+        } else {
+            for (int l = 0; l < N - base; ++l) S = S + readlane_f64(x, l);
+        }
+        x = xn;
+    }
+    double c = 0.0;
+    x = (lane < N) ? w[lane] : 0.0;
+    for (int base = 0; base < N; base += 64) {
+        const double xn = (base + 64 + lane < N) ? w[base + 64 + lane] : 0.0;
+        const double q = x / S;
+        if (base + 64 <= N) {
+#pragma unroll
+            for (int l = 0; l < 64; ++l) c = c + readlane_f64(q, l);
+        } else {
+            for (int l = 0; l < N - base; ++l) c = c + readlane_f64(q, l);
+        }
+        x = xn;
+    }
+    const double last = c;
+    const double rl = 1.0 / last;
+    const double ulo = U * (1.0 - 0x1.0p-49), uhi = U * (1.0 + 0x1.0p-49);   // |c*rl - c/last| <= 2 ulp
+    int ans = N - 1;
+    bool found = !need;
+    c = 0.0;
+    x = (lane < N) ? w[lane] : 0.0;
+    for (int base = 0; base < N; base += 64) {
+        if (__all(found)) break;
+        const double xn = (base + 64 + lane < N) ? w[base + 64 + lane] : 0.0;
+        const double q = x / S;
+        const int n = min(64, N - base);
+        for (int l = 0; l < n; ++l) {
+            c = c + readlane_f64(q, l);
+            const double r = c * rl;
+            if (!found && r > ulo) {
+                if (r > uhi || c / last > U) { found = true; ans = base + l; }
+            }
+        }
+        x = xn;
+    }
+    return ans;
 }
 
 }  // namespace epipf

@@ -28,7 +28,7 @@ __device__ __forceinline__ unsigned long long* counter_slot(unsigned long long* 
 struct StepArgs {
     int N, T, B, wg, max_chains, resample_mode, count_events, lf_max;
     size_t hist_stride, anc_stride, wstride, bstride;
-    double delta;                 // certification half-width of the parallel CDF
+    double cert_k;                // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp)
     const double* Y;
     const double* lf;
     const ChainParam* cp;
@@ -66,7 +66,7 @@ struct SimArgs {
 
 struct ResampleArgs {
     int N, B;
-    double delta;
+    double cert_k;
     const double* w;
     const double* u;
     double* wraw;

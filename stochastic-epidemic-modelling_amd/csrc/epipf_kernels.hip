@@ -121,9 +121,11 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
 
     int nev = 0, iters = 0;
     double w = 0.0;
+    // (d) multinomial (or systematic) draw and certified search, pmcmc.py:188-190
+    double U = 0.0;
+    int anc = 0;
+    bool certified = true;
     if (j < a.N) {
-        // (d) multinomial (or systematic) draw and certified search, pmcmc.py:188-190
-        double U;
         const uint32_t rtag = ((uint32_t)p & 0xFFFFFFu) | kDomainResample;
         if (a.resample_mode == 0) {
             const Block r = philox(0u, (uint32_t)j, rtag, cp.f, cp.k0, cp.k1);
@@ -132,10 +134,17 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
             const Block r = philox(0u, 0u, rtag, cp.f, cp.k0, cp.k1);
             U = ((double)j + u01(r.x, r.y)) / (double)a.N;
         }
-        bool fb;
-        int anc = resample_search<WG>(U, bpex, bsum, a.B, total, a.wloc + wprev, a.wraw + wprev, a.N, a.delta, fb);
+        anc = resample_search<WG>(U, bpex, bsum, a.B, total, a.wloc + wprev, a.N, a.cert_k, certified);
+    }
+    if (__any(!certified)) {   // wave-uniform: the whole wave resolves its uncertified draws exactly
+        const int e = resample_exact_wave(!certified, U, a.wraw + wprev, a.N);
+        if (!certified) {
+            anc = e;
+            atomicAdd(counter_slot(a.counters) + 1, 1ull);
+        }
+    }
+    if (j < a.N) {
         anc = min(max(anc, 0), a.N - 1);
-        if (fb) atomicAdd(counter_slot(a.counters) + 1, 1ull);
         a.ancestry[(size_t)chain * a.anc_stride + (size_t)p * a.N + j] = anc;   // :193
         // (f) gather the parent state, (g) propagate over [0, 1], :195-220
         const int32_t* hp = a.hidden + (size_t)chain * a.hist_stride + ((size_t)(p - 1) * a.N + anc) * C;
@@ -233,12 +242,18 @@ __global__ __launch_bounds__(WG) void resample_search_kernel(ResampleArgs a) {
         if (j == 0) *a.status = 1;
         return;
     }
-    if (j < a.N) {
-        bool fb;
-        const int anc = resample_search<WG>(a.u[j], bpex, bsum, a.B, total, a.wloc, a.wraw, a.N, a.delta, fb);
-        a.out[j] = min(max(anc, 0), a.N - 1);
-        if (fb) atomicAdd(a.fallbacks, 1ull);
+    const double U = (j < a.N) ? a.u[j] : 0.0;
+    bool certified = true;
+    int anc = 0;
+    if (j < a.N) anc = resample_search<WG>(U, bpex, bsum, a.B, total, a.wloc, a.N, a.cert_k, certified);
+    if (__any(!certified)) {
+        const int e = resample_exact_wave(!certified, U, a.wraw, a.N);
+        if (!certified) {
+            anc = e;
+            atomicAdd(a.fallbacks, 1ull);
+        }
     }
+    if (j < a.N) a.out[j] = min(max(anc, 0), a.N - 1);
 }
 
 // ------------------------------------------------------------------------------- launchers

@@ -159,13 +159,14 @@ def test_resample_matches_numpy_choice(kernels_golden, n):
     np.testing.assert_array_equal(out, rec["expected"])
 
 
-def test_resample_ties_take_the_exact_path():
+@pytest.mark.parametrize("n", [3000, 4097, 20001])
+def test_resample_ties_take_the_exact_path(n):
     """Uniforms placed exactly on (and one ulp around) numpy's CDF boundaries: the certified search must
-    hand them to the sequential path and still equal numpy's answer."""
+    hand them to the wave-cooperative exact path (many such lanes per wave, ragged last chunk) and still
+    equal numpy's answer."""
     from epipf.engine import get_engine
     eng = get_engine("sir", 1, 8, 2, 1)
-    rs = np.random.RandomState(5)
-    n = 3000
+    rs = np.random.RandomState(5 + n)
     w = rs.random_sample(n) ** 4
     w[rs.random_sample(n) < 0.2] = 0.0
     p = w / sum(w)
