@@ -37,10 +37,20 @@ __device__ __forceinline__ Block philox(uint32_t c0, uint32_t c1, uint32_t c2, u
     return Block{c0, c1, c2, c3};
 }
 
-// 53-bit uniform in [0, 1): ((hi << 32 | lo) >> 11) * 2^-53  (numpy's Philox double convention)
+// 53-bit uniform in [0, 1): ((hi << 32 | lo) >> 11) * 2^-53  (numpy's Philox double convention).
+// With m = (hi:lo) >> 11 split as mh = hi >> 11 (21 bits) and ml = low 32 bits of m, U = mh 2^-21 + ml 2^-53:
+// both conversions and the scaling are exact and the fused add of two exact terms whose sum is representable
+// is exact, so this equals the 64-bit shift + convert form bit for bit (two 32-bit converts, no 64-bit ops).
 __device__ __forceinline__ double u01(uint32_t lo, uint32_t hi) {
-    const uint64_t v = ((uint64_t)hi << 32) | lo;
-    return (double)(v >> 11) * 0x1.0p-53;
+    const uint32_t mh = hi >> 11, ml = __builtin_amdgcn_alignbit(hi, lo, 11);
+    return fma((double)mh, 0x1.0p-21, (double)ml * 0x1.0p-53);
+}
+
+// 1 - U for the same U, exactly: 1 - mh 2^-21 is a multiple of 2^-21 in (0, 1] and the final fused add
+// subtracts an exact term from it with a representable result (1 - U = (2^53 - m) 2^-53).
+__device__ __forceinline__ double one_minus_u01(uint32_t lo, uint32_t hi) {
+    const uint32_t mh = hi >> 11, ml = __builtin_amdgcn_alignbit(hi, lo, 11);
+    return fma((double)ml, -0x1.0p-53, fma((double)mh, -0x1.0p-21, 1.0));
 }
 
 // ------------------------------------------------------------------------------- per-chain parameters
@@ -73,28 +83,55 @@ __device__ __forceinline__ void log_table_entry(LogTab* tab, int i) {
     }
 }
 
-__device__ __forceinline__ double fast_log(double x, const LogTab* __restrict__ tab) {
-    const uint64_t ix = (uint64_t)__double_as_longlong(x);
-    const uint64_t tmp = ix - kLogOff;
-    const int i = (int)((tmp >> 45) & 127);
-    const bool near1 = fabs(x - 1.0) < 0x1.0p-8;
+// Index, exponent and reduced argument are formed on the high 32-bit word (kLogOff's low word is zero, so
+// ix - kLogOff never borrows); inputs within 2^-8 of 1 select the exact {1, 0} bin with k = 0, z = x, so
+// r = x - 1 exactly -- no branch.
+// P(r) = 1/7 r^5 - 1/6 r^4 + 1/5 r^3 - 1/4 r^2 + 1/3 r - 1/2 by Horner, as five dependent three-operand
+// v_fma_f64 with the constants in SGPR pairs, in one asm block: hipcc otherwise copies each constant into
+// the destination of a two-address v_fmac_f64 (one 64-bit move per step), and separate asm statements get
+// an s_nop between them.  VALU-to-VALU dependencies need no wait states.
+__device__ __forceinline__ double log1p_horner(double r) {
+    double p;
+    asm("v_fma_f64 %0, %1, %2, %3\n\t"
+        "v_fma_f64 %0, %1, %0, %4\n\t"
+        "v_fma_f64 %0, %1, %0, %5\n\t"
+        "v_fma_f64 %0, %1, %0, %6\n\t"
+        "v_fma_f64 %0, %1, %0, %7"
+        : "=&v"(p)
+        : "v"(r), "v"(1.0 / 7.0), "s"(-1.0 / 6.0), "s"(1.0 / 5.0), "s"(-0.25), "s"(1.0 / 3.0), "s"(-0.5));
+    return p;
+}
+
+constexpr int kLogOneBin = (int)(((0x3FF00000u - 0x3FE60000u) >> 13) & 127);   // bin holding 1.0
+
+__device__ __forceinline__ double fast_log_sel(double x, bool near1, const LogTab* __restrict__ tab) {
+    const long long ix = __double_as_longlong(x);
+    const uint32_t hi = (uint32_t)(ix >> 32);
+    const int lo = (int)ix;
+    const uint32_t th = hi - (uint32_t)(kLogOff >> 32);
+    const int i = near1 ? kLogOneBin : (int)((th >> 13) & 127);
+    const int k = near1 ? 0 : ((int)th >> 20);
+    const uint32_t zh = near1 ? hi : hi - (th & 0xFFF00000u);
+    const double z = __hiloint2double((int)zh, lo);
     const LogTab e = tab[i];
-    const int k = near1 ? 0 : (int)((int64_t)tmp >> 52);
-    const double z = near1 ? x : __longlong_as_double((long long)(ix - (tmp & (0xFFFull << 52))));
-    const double ic = near1 ? 1.0 : e.invc, lc = near1 ? 0.0 : e.logc;
-    const double r = fma(z, ic, -1.0);
+    const double r = fma(z, e.invc, -1.0);
     const double kd = (double)k;
-    const double w = fma(kd, 0x1.62e42fefa3800p-1, lc);           // k*ln2_hi + log c (exact product)
-    const double hi = w + r;
-    double lo = (w - hi) + r;
-    lo = fma(kd, 0x1.ef35793c76730p-45, lo);                      // k*ln2_lo
-    double p = 1.0 / 7.0;
-    p = fma(r, p, -1.0 / 6.0);
-    p = fma(r, p, 1.0 / 5.0);
-    p = fma(r, p, -0.25);
-    p = fma(r, p, 1.0 / 3.0);
-    p = fma(r, p, -0.5);
-    return hi + fma(r * r, p, lo);                                // log1p(r) = r + r^2 P(r)
+    const double w = fma(kd, 0x1.62e42fefa3800p-1, e.logc);       // k*ln2_hi + log c (exact product)
+    const double hs = w + r;
+    double ls = (w - hs) + r;
+    ls = fma(kd, 0x1.ef35793c76730p-45, ls);                      // k*ln2_lo
+    const double p = log1p_horner(r);
+    return hs + fma(r * r, p, ls);                                // log1p(r) = r + r^2 P(r)
+}
+
+__device__ __forceinline__ double fast_log(double x, const LogTab* __restrict__ tab) {
+    return fast_log_sel(x, fabs(x - 1.0) < 0x1.0p-8, tab);
+}
+
+// -log(1 - U), U = u01(lo, hi): the reference's np.random.exponential(1) (gillespie_algo.py:62).
+// |(1 - U) - 1| = U < 2^-8  <=>  m < 2^45  <=>  hi >> 11 < 2^13, so the near-1 test is one integer compare.
+__device__ __forceinline__ double neg_log_one_minus_u01(uint32_t lo, uint32_t hi, const LogTab* __restrict__ tab) {
+    return -fast_log_sel(one_minus_u01(lo, hi), (hi >> 11) < 8192u, tab);
 }
 
 // 1/a to ~1 ulp: hardware reciprocal + two Newton steps
@@ -108,6 +145,8 @@ __device__ __forceinline__ double recip(double a) {
 // Direct method over [0, tmax] from state x (integers held in doubles, as the reference holds them),
 // gillespie_algo.py.  Event k of this lane draws Philox block (k, j, ptag, f): tau from (x,y), the
 // channel from (z,w).  Both uniforms are consumed before the overshoot test, as in the reference.
+// Every lane still in the loop is at the same event index k (all start at 0 and step together), so k is
+// read wave-uniform: Philox's first round (and half of its second) then runs on the scalar unit.
 //
 // Fast path + certified fallback: the channel decision of the reference is
 //   count_i [ fl(c_i / c_last) <= u ],  c = cumsum(fl(a_l / sum(a)))            (numpy choice, :63)
@@ -160,18 +199,23 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
     double t = 0.0;
     uint32_t k = 0;
     int nev = 0;
+    // Software pipelining: event k+1's Philox block (counter-based, so independent of event k's outcome) is
+    // computed while event k's f64 work runs, which gives each wave two independent dependency chains.  The
+    // block drawn after the last event is discarded (one per particle-step).
+    Block rn = philox(0u, j, ptag, cp.f, cp.k0, cp.k1);
     if constexpr (MODEL == kSIR) {
         const double beta = cp.theta[0], gamma = cp.theta[1];
         double S = x[0], I = x[1], R = x[2];
         const double N = (S + I) + R;                                  // gillespie_algo.py:35
         const double invN = 1.0 / N;
         while (I > 0.0) {                                              // :48
-            const Block r = philox(k, j, ptag, cp.f, cp.k0, cp.k1);
+            const Block r = rn;                                        // this event's block
             ++k;
+            rn = philox(__builtin_amdgcn_readfirstlane(k), j, ptag, cp.f, cp.k0, cp.k1);   // next event's
             const double a0 = ((beta * S) * I) * invN;                 // :38
             const double as = a0 + gamma * I;                          // :39
             const double ri = recip(as);
-            const double tau = ri * (-fast_log(1.0 - u01(r.x, r.y), tab));   // np.random.exponential, :62
+            const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);   // np.random.exponential, :62
             const double u = u01(r.z, r.w);
             const double q = a0 * ri;
             bool second = q <= u;                                      // choice(2, p=a/sum(a)), :63
@@ -188,12 +232,13 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
         const double N = ((S + E) + I) + R;                            // :104
         const double invN = 1.0 / N;
         while (E > 0.0 || I > 0.0) {                                   // :119
-            const Block r = philox(k, j, ptag, cp.f, cp.k0, cp.k1);
+            const Block r = rn;                                        // this event's block
             ++k;
+            rn = philox(__builtin_amdgcn_readfirstlane(k), j, ptag, cp.f, cp.k0, cp.k1);   // next event's
             const double a0 = ((beta * S) * I) * invN, a01 = a0 + alpha * E;
             const double as = a01 + gamma * I;
             const double ri = recip(as);
-            const double tau = ri * (-fast_log(1.0 - u01(r.x, r.y), tab));   // :133
+            const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);   // :133
             const double u = u01(r.z, r.w);
             const double q0 = a0 * ri, q1 = a01 * ri;
             int ch = (q0 <= u ? 1 : 0) + (q1 <= u ? 1 : 0);            // :134
@@ -222,8 +267,9 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
 #pragma unroll
         for (int g = 0; g < G; ++g) infected = infected + I[g];        // :192
         while (infected > 0.0) {                                       // :193
-            const Block r = philox(k, j, ptag, cp.f, cp.k0, cp.k1);
+            const Block r = rn;                                        // this event's block
             ++k;
+            rn = philox(__builtin_amdgcn_readfirstlane(k), j, ptag, cp.f, cp.k0, cp.k1);   // next event's
             double cum[NCH];
             double run = 0.0;
 #pragma unroll
@@ -237,7 +283,7 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
                 cum[g * (G + 1) + G] = run;
             }
             const double ri = recip(run);
-            const double tau = ri * (-fast_log(1.0 - u01(r.x, r.y), tab));
+            const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);
             const double u = u01(r.z, r.w);
             int ch = 0;
             bool close = false;
