@@ -203,40 +203,51 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
     // computed while event k's f64 work runs, which gives each wave two independent dependency chains.  The
     // block drawn after the last event is discarded (one per particle-step).
     Block rn = philox(0u, j, ptag, cp.f, cp.k0, cp.k1);
+    // Propensities are formed as (beta/N) * (S*I) and fma(gamma, I, a0): within a few ulps of the reference's
+    // ((beta*S)*I)/N and a0 + gamma*I, which the 2^-44 channel band and the ulp-level tau tolerance absorb
+    // (DESIGN.md §4).  One exit test per event: the overshoot and the absorbing state are folded into `alive`.
     if constexpr (MODEL == kSIR) {
         const double beta = cp.theta[0], gamma = cp.theta[1];
         double S = x[0], I = x[1], R = x[2];
         const double N = (S + I) + R;                                  // gillespie_algo.py:35
-        const double invN = 1.0 / N;
-        while (I > 0.0) {                                              // :48
+        const double bN = beta / N;
+        bool alive = I > 0.0;                                          // :48
+        while (alive) {
             const Block r = rn;                                        // this event's block
             ++k;
             rn = philox(__builtin_amdgcn_readfirstlane(k), j, ptag, cp.f, cp.k0, cp.k1);   // next event's
-            const double a0 = ((beta * S) * I) * invN;                 // :38
-            const double as = a0 + gamma * I;                          // :39
+            const double a0 = bN * (S * I);                            // :38
+            const double as = fma(gamma, I, a0);                       // :39
             const double ri = recip(as);
             const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);   // np.random.exponential, :62
             const double u = u01(r.z, r.w);
             const double q = a0 * ri;
             bool second = q <= u;                                      // choice(2, p=a/sum(a)), :63
             if (fabs(q - u) <= kBand) second = sir_channel_exact(beta, gamma, S, I, N, u);
-            if (t + tau > tmax) break;                                 // :65-66
-            t = t + tau;
-            if (second) { I -= 1.0; R += 1.0; } else { S -= 1.0; I += 1.0; }
-            ++nev;
+            const double tn = t + tau;
+            alive = !(tn > tmax);                                      // :65-66
+            if (alive) {
+                t = tn;
+                S = second ? S : S - 1.0;
+                R = second ? R + 1.0 : R;
+                I = second ? I - 1.0 : I + 1.0;
+                ++nev;
+                alive = I > 0.0;
+            }
         }
         x[0] = S; x[1] = I; x[2] = R;
     } else if constexpr (MODEL == kSEIR) {
         const double beta = cp.theta[0], alpha = cp.theta[1], gamma = cp.theta[2];   // :92
         double S = x[0], E = x[1], I = x[2], R = x[3];
         const double N = ((S + E) + I) + R;                            // :104
-        const double invN = 1.0 / N;
-        while (E > 0.0 || I > 0.0) {                                   // :119
+        const double bN = beta / N;
+        bool alive = E > 0.0 || I > 0.0;                               // :119
+        while (alive) {
             const Block r = rn;                                        // this event's block
             ++k;
             rn = philox(__builtin_amdgcn_readfirstlane(k), j, ptag, cp.f, cp.k0, cp.k1);   // next event's
-            const double a0 = ((beta * S) * I) * invN, a01 = a0 + alpha * E;
-            const double as = a01 + gamma * I;
+            const double a0 = bN * (S * I), a01 = fma(alpha, E, a0);
+            const double as = fma(gamma, I, a01);
             const double ri = recip(as);
             const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);   // :133
             const double u = u01(r.z, r.w);
@@ -244,12 +255,17 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
             int ch = (q0 <= u ? 1 : 0) + (q1 <= u ? 1 : 0);            // :134
             if (fabs(q0 - u) <= kBand || fabs(q1 - u) <= kBand)
                 ch = seir_channel_exact(beta, alpha, gamma, S, E, I, N, u);
-            if (t + tau > tmax) break;                                 // :136-137
-            t = t + tau;
-            if (ch == 0) { S -= 1.0; E += 1.0; }
-            else if (ch == 1) { E -= 1.0; I += 1.0; }
-            else { I -= 1.0; R += 1.0; }
-            ++nev;
+            const double tn = t + tau;
+            alive = !(tn > tmax);                                      // :136-137
+            if (alive) {
+                t = tn;
+                S = (ch == 0) ? S - 1.0 : S;
+                E = (ch == 0) ? E + 1.0 : (ch == 1) ? E - 1.0 : E;
+                I = (ch == 1) ? I + 1.0 : (ch == 2) ? I - 1.0 : I;
+                R = (ch == 2) ? R + 1.0 : R;
+                ++nev;
+                alive = E > 0.0 || I > 0.0;
+            }
         }
         x[0] = S; x[1] = E; x[2] = I; x[3] = R;
     } else {
@@ -266,7 +282,8 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
         double infected = 0.0;
 #pragma unroll
         for (int g = 0; g < G; ++g) infected = infected + I[g];        // :192
-        while (infected > 0.0) {                                       // :193
+        bool alive = infected > 0.0;                                   // :193
+        while (alive) {
             const Block r = rn;                                        // this event's block
             ++k;
             rn = philox(__builtin_amdgcn_readfirstlane(k), j, ptag, cp.f, cp.k0, cp.k1);   // next event's
@@ -274,12 +291,13 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
             double run = 0.0;
 #pragma unroll
             for (int g = 0; g < G; ++g) {                              // channel order, :180-185
+                const double cI = I[g] * invSumN;
 #pragma unroll
                 for (int g2 = 0; g2 < G; ++g2) {
-                    run = run + ((cp.theta[g * G + g2] * S[g2]) * I[g]) * invSumN;
+                    run = fma(cp.theta[g * G + g2] * S[g2], cI, run);
                     cum[g * (G + 1) + g2] = run;
                 }
-                run = run + gamma * I[g];
+                run = fma(gamma, I[g], run);
                 cum[g * (G + 1) + G] = run;
             }
             const double ri = recip(run);
@@ -294,19 +312,23 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
                 close |= fabs(q - u) <= kBand;
             }
             if (close) ch = subgroups_channel_exact<G>(cp.theta, S, I, sumN, u);
-            if (t + tau > tmax) break;                                 // :215-216
-            t = t + tau;
+            const double tn = t + tau;
+            alive = !(tn > tmax);                                      // :215-216
+            if (alive) {
+                t = tn;
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
+                for (int g = 0; g < G; ++g) {
 #pragma unroll
-                for (int g2 = 0; g2 < G; ++g2)
-                    if (ch == g * (G + 1) + g2) { S[g2] -= 1.0; I[g2] += 1.0; }   // s_{g}_{g2}: :183
-                if (ch == g * (G + 1) + G) { I[g] -= 1.0; R[g] += 1.0; }         // i_{g}: :185
+                    for (int g2 = 0; g2 < G; ++g2)
+                        if (ch == g * (G + 1) + g2) { S[g2] -= 1.0; I[g2] += 1.0; }   // s_{g}_{g2}: :183
+                    if (ch == g * (G + 1) + G) { I[g] -= 1.0; R[g] += 1.0; }         // i_{g}: :185
+                }
+                ++nev;
+                infected = 0.0;
+#pragma unroll
+                for (int g = 0; g < G; ++g) infected = infected + I[g];   // :222
+                alive = infected > 0.0;
             }
-            ++nev;
-            infected = 0.0;
-#pragma unroll
-            for (int g = 0; g < G; ++g) infected = infected + I[g];    // :222
         }
 #pragma unroll
         for (int g = 0; g < G; ++g) { x[3 * g] = S[g]; x[3 * g + 1] = I[g]; x[3 * g + 2] = R[g]; }
