@@ -32,7 +32,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--chains", type=int, default=int(os.environ.get("EPIPF_BENCH_CHAINS", 32)),
+    ap.add_argument("--chains", type=int, default=int(os.environ.get("EPIPF_BENCH_CHAINS", 128)),
                     help="independent MH chains per GPU (batched in one launch per filter step)")
     ap.add_argument("--particles", type=int, default=10000)
     ap.add_argument("--config", type=int, default=2)

@@ -211,6 +211,7 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
         double S = x[0], I = x[1], R = x[2];
         const double N = (S + I) + R;                                  // gillespie_algo.py:35
         const double bN = beta / N;
+        int nrec = 0;
         bool alive = I > 0.0;                                          // :48
         while (alive) {
             const Block r = rn;                                        // this event's block
@@ -226,16 +227,16 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
             if (fabs(q - u) <= kBand) second = sir_channel_exact(beta, gamma, S, I, N, u);
             const double tn = t + tau;
             alive = !(tn > tmax);                                      // :65-66
-            if (alive) {
+            if (alive) {                                               // :68-70; R is not needed in the loop
                 t = tn;
-                S = second ? S : S - 1.0;
-                R = second ? R + 1.0 : R;
-                I = second ? I - 1.0 : I + 1.0;
+                S = S + (second ? 0.0 : -1.0);
+                I = I + (second ? -1.0 : 1.0);
+                nrec += second ? 1 : 0;
                 ++nev;
                 alive = I > 0.0;
             }
         }
-        x[0] = S; x[1] = I; x[2] = R;
+        x[0] = S; x[1] = I; x[2] = R + (double)nrec;
     } else if constexpr (MODEL == kSEIR) {
         const double beta = cp.theta[0], alpha = cp.theta[1], gamma = cp.theta[2];   // :92
         double S = x[0], E = x[1], I = x[2], R = x[3];
