@@ -193,147 +193,172 @@ __device__ __forceinline__ int subgroups_channel_exact(const double* th, const d
     return ch;
 }
 
+// Per-model event state: load() from the compartment counts, active() = the reference's loop condition,
+// event(r) = one pass of the reference's loop body with Philox block r (returns false, state untouched, when
+// the event overshoots tmax: the reference's break), save() back to counts.
+//
+// Propensities are formed as (beta/N) * (S*I) and with fused sums: within a few ulps of the reference's
+// ((beta*S)*I)/N and a0 + gamma*I, which the 2^-44 channel band and the ulp-level tau tolerance absorb
+// (DESIGN.md §4).
 template <int MODEL, int G>
-__device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
-                                             double tmax, const LogTab* __restrict__ tab, int& iters) {
-    double t = 0.0;
-    uint32_t k = 0;
-    int nev = 0;
-    // Software pipelining: event k+1's Philox block (counter-based, so independent of event k's outcome) is
-    // computed while event k's f64 work runs, which gives each wave two independent dependency chains.  The
-    // block drawn after the last event is discarded (one per particle-step).
-    Block rn = philox(0u, j, ptag, cp.f, cp.k0, cp.k1);
-    // Propensities are formed as (beta/N) * (S*I) and fma(gamma, I, a0): within a few ulps of the reference's
-    // ((beta*S)*I)/N and a0 + gamma*I, which the 2^-44 channel band and the ulp-level tau tolerance absorb
-    // (DESIGN.md §4).  One exit test per event: the overshoot and the absorbing state are folded into `alive`.
-    if constexpr (MODEL == kSIR) {
-        const double beta = cp.theta[0], gamma = cp.theta[1];
-        double S = x[0], I = x[1], R = x[2];
-        const double N = (S + I) + R;                                  // gillespie_algo.py:35
-        const double bN = beta / N;
-        int nrec = 0;
-        bool alive = I > 0.0;                                          // :48
-        while (alive) {
-            const Block r = rn;                                        // this event's block
-            ++k;
-            rn = philox(__builtin_amdgcn_readfirstlane(k), j, ptag, cp.f, cp.k0, cp.k1);   // next event's
-            const double a0 = bN * (S * I);                            // :38
-            const double as = fma(gamma, I, a0);                       // :39
-            const double ri = recip(as);
-            const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);   // np.random.exponential, :62
-            const double u = u01(r.z, r.w);
-            const double q = a0 * ri;
-            bool second = q <= u;                                      // choice(2, p=a/sum(a)), :63
-            if (fabs(q - u) <= kBand) second = sir_channel_exact(beta, gamma, S, I, N, u);
-            const double tn = t + tau;
-            alive = !(tn > tmax);                                      // :65-66
-            if (alive) {                                               // :68-70; R is not needed in the loop
-                t = tn;
-                S = S + (second ? 0.0 : -1.0);
-                I = I + (second ? -1.0 : 1.0);
-                nrec += second ? 1 : 0;
-                ++nev;
-                alive = I > 0.0;
-            }
-        }
-        x[0] = S; x[1] = I; x[2] = R + (double)nrec;
-    } else if constexpr (MODEL == kSEIR) {
-        const double beta = cp.theta[0], alpha = cp.theta[1], gamma = cp.theta[2];   // :92
-        double S = x[0], E = x[1], I = x[2], R = x[3];
-        const double N = ((S + E) + I) + R;                            // :104
-        const double bN = beta / N;
-        bool alive = E > 0.0 || I > 0.0;                               // :119
-        while (alive) {
-            const Block r = rn;                                        // this event's block
-            ++k;
-            rn = philox(__builtin_amdgcn_readfirstlane(k), j, ptag, cp.f, cp.k0, cp.k1);   // next event's
-            const double a0 = bN * (S * I), a01 = fma(alpha, E, a0);
-            const double as = fma(gamma, I, a01);
-            const double ri = recip(as);
-            const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);   // :133
-            const double u = u01(r.z, r.w);
-            const double q0 = a0 * ri, q1 = a01 * ri;
-            int ch = (q0 <= u ? 1 : 0) + (q1 <= u ? 1 : 0);            // :134
-            if (fabs(q0 - u) <= kBand || fabs(q1 - u) <= kBand)
-                ch = seir_channel_exact(beta, alpha, gamma, S, E, I, N, u);
-            const double tn = t + tau;
-            alive = !(tn > tmax);                                      // :136-137
-            if (alive) {
-                t = tn;
-                S = (ch == 0) ? S - 1.0 : S;
-                E = (ch == 0) ? E + 1.0 : (ch == 1) ? E - 1.0 : E;
-                I = (ch == 1) ? I + 1.0 : (ch == 2) ? I - 1.0 : I;
-                R = (ch == 2) ? R + 1.0 : R;
-                ++nev;
-                alive = E > 0.0 || I > 0.0;
-            }
-        }
-        x[0] = S; x[1] = E; x[2] = I; x[3] = R;
-    } else {
-        constexpr int NCH = G * G + G;
-        const double gamma = cp.theta[G * G];
-        double S[G], I[G], R[G];
-        double sumN = 0.0;
+struct SsaState;
+
+template <>
+struct SsaState<kSIR, 1> {                                             // gillespie_algo.py:10-75
+    double S, I, R, N, bN;
+    int nrec;
+    __device__ __forceinline__ void load(const double* x, const ChainParam& cp) {
+        S = x[0]; I = x[1]; R = x[2];
+        N = (S + I) + R;                                               // :35
+        bN = cp.theta[0] / N;
+        nrec = 0;
+    }
+    __device__ __forceinline__ bool active() const { return I > 0.0; }   // :48
+    __device__ __forceinline__ bool event(const Block& r, double& t, double tmax, const ChainParam& cp,
+                                          const LogTab* __restrict__ tab) {
+        const double gamma = cp.theta[1];
+        const double a0 = bN * (S * I);                                // :38
+        const double as = fma(gamma, I, a0);                           // :39
+        const double ri = recip(as);
+        const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);  // np.random.exponential, :62
+        const double u = u01(r.z, r.w);
+        const double q = a0 * ri;
+        bool second = q <= u;                                          // choice(2, p=a/sum(a)), :63
+        if (fabs(q - u) <= kBand) second = sir_channel_exact(cp.theta[0], gamma, S, I, N, u);
+        const double tn = t + tau;
+        if (tn > tmax) return false;                                   // :65-66
+        t = tn;                                                        // :68-70; R is not needed in the loop
+        S = S + (second ? 0.0 : -1.0);
+        I = I + (second ? -1.0 : 1.0);
+        nrec += second ? 1 : 0;
+        return true;
+    }
+    __device__ __forceinline__ void save(double* x) const { x[0] = S; x[1] = I; x[2] = R + (double)nrec; }
+};
+
+template <>
+struct SsaState<kSEIR, 1> {                                            // gillespie_algo.py:78-146
+    double S, E, I, R, N, bN;
+    __device__ __forceinline__ void load(const double* x, const ChainParam& cp) {
+        S = x[0]; E = x[1]; I = x[2]; R = x[3];
+        N = ((S + E) + I) + R;                                         // :104
+        bN = cp.theta[0] / N;                                          // theta = (beta, alpha, gamma), :92
+    }
+    __device__ __forceinline__ bool active() const { return E > 0.0 || I > 0.0; }   // :119
+    __device__ __forceinline__ bool event(const Block& r, double& t, double tmax, const ChainParam& cp,
+                                          const LogTab* __restrict__ tab) {
+        const double alpha = cp.theta[1], gamma = cp.theta[2];
+        const double a0 = bN * (S * I), a01 = fma(alpha, E, a0);       // :107-109
+        const double as = fma(gamma, I, a01);
+        const double ri = recip(as);
+        const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);  // :133
+        const double u = u01(r.z, r.w);
+        const double q0 = a0 * ri, q1 = a01 * ri;
+        int ch = (q0 <= u ? 1 : 0) + (q1 <= u ? 1 : 0);                // :134
+        if (fabs(q0 - u) <= kBand || fabs(q1 - u) <= kBand)
+            ch = seir_channel_exact(cp.theta[0], alpha, gamma, S, E, I, N, u);
+        const double tn = t + tau;
+        if (tn > tmax) return false;                                   // :136-137
+        t = tn;
+        S = (ch == 0) ? S - 1.0 : S;
+        E = (ch == 0) ? E + 1.0 : (ch == 1) ? E - 1.0 : E;
+        I = (ch == 1) ? I + 1.0 : (ch == 2) ? I - 1.0 : I;
+        R = (ch == 2) ? R + 1.0 : R;
+        return true;
+    }
+    __device__ __forceinline__ void save(double* x) const { x[0] = S; x[1] = E; x[2] = I; x[3] = R; }
+};
+
+template <int G>
+struct SubgroupsState {                                                // gillespie_algo.py:148-233
+    static constexpr int NCH = G * G + G;
+    double S[G], I[G], R[G], sumN, invSumN;
+    __device__ __forceinline__ void load(const double* x, const ChainParam&) {
+        sumN = 0.0;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             S[g] = x[3 * g]; I[g] = x[3 * g + 1]; R[g] = x[3 * g + 2];
             sumN = sumN + ((S[g] + I[g]) + R[g]);                      // sum(N), :176,:182
         }
-        const double invSumN = 1.0 / sumN;
+        invSumN = 1.0 / sumN;
+    }
+    __device__ __forceinline__ bool active() const {                   // :192-193, :222
         double infected = 0.0;
 #pragma unroll
-        for (int g = 0; g < G; ++g) infected = infected + I[g];        // :192
-        bool alive = infected > 0.0;                                   // :193
-        while (alive) {
-            const Block r = rn;                                        // this event's block
-            ++k;
-            rn = philox(__builtin_amdgcn_readfirstlane(k), j, ptag, cp.f, cp.k0, cp.k1);   // next event's
-            double cum[NCH];
-            double run = 0.0;
+        for (int g = 0; g < G; ++g) infected = infected + I[g];
+        return infected > 0.0;
+    }
+    __device__ __forceinline__ bool event(const Block& r, double& t, double tmax, const ChainParam& cp,
+                                          const LogTab* __restrict__ tab) {
+        const double gamma = cp.theta[G * G];
+        double cum[NCH];
+        double run = 0.0;
 #pragma unroll
-            for (int g = 0; g < G; ++g) {                              // channel order, :180-185
-                const double cI = I[g] * invSumN;
+        for (int g = 0; g < G; ++g) {                                  // channel order, :180-185
+            const double cI = I[g] * invSumN;
 #pragma unroll
-                for (int g2 = 0; g2 < G; ++g2) {
-                    run = fma(cp.theta[g * G + g2] * S[g2], cI, run);
-                    cum[g * (G + 1) + g2] = run;
-                }
-                run = fma(gamma, I[g], run);
-                cum[g * (G + 1) + G] = run;
+            for (int g2 = 0; g2 < G; ++g2) {
+                run = fma(cp.theta[g * G + g2] * S[g2], cI, run);
+                cum[g * (G + 1) + g2] = run;
             }
-            const double ri = recip(run);
-            const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);
-            const double u = u01(r.z, r.w);
-            int ch = 0;
-            bool close = false;
-#pragma unroll
-            for (int i = 0; i < NCH - 1; ++i) {
-                const double q = cum[i] * ri;
-                ch += (q <= u) ? 1 : 0;
-                close |= fabs(q - u) <= kBand;
-            }
-            if (close) ch = subgroups_channel_exact<G>(cp.theta, S, I, sumN, u);
-            const double tn = t + tau;
-            alive = !(tn > tmax);                                      // :215-216
-            if (alive) {
-                t = tn;
-#pragma unroll
-                for (int g = 0; g < G; ++g) {
-#pragma unroll
-                    for (int g2 = 0; g2 < G; ++g2)
-                        if (ch == g * (G + 1) + g2) { S[g2] -= 1.0; I[g2] += 1.0; }   // s_{g}_{g2}: :183
-                    if (ch == g * (G + 1) + G) { I[g] -= 1.0; R[g] += 1.0; }         // i_{g}: :185
-                }
-                ++nev;
-                infected = 0.0;
-#pragma unroll
-                for (int g = 0; g < G; ++g) infected = infected + I[g];   // :222
-                alive = infected > 0.0;
-            }
+            run = fma(gamma, I[g], run);
+            cum[g * (G + 1) + G] = run;
         }
+        const double ri = recip(run);
+        const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);
+        const double u = u01(r.z, r.w);
+        int ch = 0;
+        bool close = false;
+#pragma unroll
+        for (int i = 0; i < NCH - 1; ++i) {
+            const double q = cum[i] * ri;
+            ch += (q <= u) ? 1 : 0;
+            close |= fabs(q - u) <= kBand;
+        }
+        if (close) ch = subgroups_channel_exact<G>(cp.theta, S, I, sumN, u);
+        const double tn = t + tau;
+        if (tn > tmax) return false;                                   // :215-216
+        t = tn;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+#pragma unroll
+            for (int g2 = 0; g2 < G; ++g2)
+                if (ch == g * (G + 1) + g2) { S[g2] -= 1.0; I[g2] += 1.0; }   // s_{g}_{g2}: :183
+            if (ch == g * (G + 1) + G) { I[g] -= 1.0; R[g] += 1.0; }         // i_{g}: :185
+        }
+        return true;
+    }
+    __device__ __forceinline__ void save(double* x) const {
 #pragma unroll
         for (int g = 0; g < G; ++g) { x[3 * g] = S[g]; x[3 * g + 1] = I[g]; x[3 * g + 2] = R[g]; }
     }
+};
+template <int G> struct SsaState<kSubgroups, G> : SubgroupsState<G> {};
+template <int G> struct SsaState<kSubgroups2, G> : SubgroupsState<G> {};
+
+// One particle over [0, tmax] (every lane of the wave starts together, so the event index k is wave-uniform).
+// Software pipelining: event k+1's Philox block (counter-based, so independent of event k's outcome) is
+// computed while event k's f64 work runs, which gives each wave two independent dependency chains.  The
+// block drawn after the last event is discarded (one per particle-step).
+template <int MODEL, int G>
+__device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
+                                             double tmax, const LogTab* __restrict__ tab, int& iters) {
+    SsaState<MODEL, G> st;
+    st.load(x, cp);
+    double t = 0.0;
+    uint32_t k = 0;
+    int nev = 0;
+    Block rn = philox(0u, j, ptag, cp.f, cp.k0, cp.k1);
+    bool alive = st.active();
+    while (alive) {
+        const Block r = rn;                                            // this event's block
+        ++k;
+        rn = philox(__builtin_amdgcn_readfirstlane(k), j, ptag, cp.f, cp.k0, cp.k1);   // next event's
+        const bool ev = st.event(r, t, tmax, cp, tab);
+        nev += ev ? 1 : 0;
+        alive = ev && st.active();
+    }
+    st.save(x);
     iters = (int)k;
     return nev;
 }
