@@ -34,7 +34,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--chains", type=int, default=int(os.environ.get("EPIPF_BENCH_CHAINS", 128)),
                     help="independent MH chains per GPU (batched in one launch per filter step)")
-    ap.add_argument("--particles", type=int, default=10000)
+    ap.add_argument("--particles", type=int, default=None, help="default: the config's N (SURVEY.md §8d)")
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
@@ -61,7 +61,10 @@ def cpu_baseline(Y, meta, N, seconds):
     threads = min(16, os.cpu_count() or 1)
     os.environ.setdefault("OMP_NUM_THREADS", str(threads))
     oracle.build()
-    th = np.array(meta["theta"])
+    th = np.array(meta["theta"], dtype=np.float64)
+    if meta["model"].startswith("sir_subgroups"):                     # (beta[G][G], gamma), pmcmc.py:289-296
+        G = int(round(np.sqrt(th.size - 1)))
+        th = (th[:G * G].reshape(G, G), th[-1])
     t0 = time.perf_counter()
     n = 0
     ev = 0
@@ -74,7 +77,7 @@ def cpu_baseline(Y, meta, N, seconds):
             break
     dt = time.perf_counter() - t0
     return dict(value=n * N * Y.shape[0] / dt, unit="particle-steps/s", cores=oracle.num_threads(), kind="port",
-                sample=f"{n} full filter(s) of config 2 (N={N}, T={Y.shape[0]}), {dt:.1f}s, {ev / dt:.3g} events/s, "
+                sample=f"{n} full filter(s) of the bench config (N={N}, T={Y.shape[0]}), {dt:.1f}s, {ev / dt:.3g} events/s, "
                        f"host CPU: {cpu_model()}")
 
 
@@ -96,7 +99,7 @@ def main():
     from epipf.pmcmc import ChainSampler, chain_key
 
     Y, meta = datasets.benchmark_dataset(args.config)
-    N, T = args.particles, Y.shape[0]
+    N, T = (args.particles or meta["N"]), Y.shape[0]
     C = args.chains
     gid = shard(C * world, world, rank)                              # global chain ids of this rank
     sampler = ChainSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=args.warmup + args.steps + 2,
@@ -149,7 +152,8 @@ def main():
     launches = max(1, st["step_launches"])
     avg_launch_s = st["step_ms"] / 1e3 / launches
     units_per_launch = filters * N / args.steps                      # particle-steps per launch (all chains)
-    bytes_per_unit = 8 * 3 + 40                                       # 8C+40 with C=3
+    n_comp = {"sir": 3, "seir": 4}.get(meta["model"], 3 * len(np.atleast_1d(meta["n_population"])))
+    bytes_per_unit = 8 * n_comp + 40                                  # 8C+40 B per particle-step
     achieved = units_per_launch * bytes_per_unit / avg_launch_s / 1e9
     traffic = None
     pmc_path = os.path.join(REPO, "profiles", "pmc_step_kernel.json")
@@ -164,6 +168,7 @@ def main():
     single = None
     if args.single_chain and rank == 0 and world == 1:
         s1 = ChainSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=args.steps + 2, probs=meta["probs"],
+                          observations=meta.get("observations", False),
                           n_particles=N, n_population=meta["n_population"], mu=meta["mu"],
                           rngs=[np.random.RandomState(args.seed)], keys=[chain_key(args.seed, 0)], device=local,
                           mh_ratio="log")
@@ -192,10 +197,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (config-2 ODE SIR y0=(9980,20,0), beta=.25, gamma=.1, 200 daily rows, "
-                    "binomial thinning p=.1, RandomState(1)); Philox-keyed filter draws",
-            "config": {"workload": f"BASELINE config {args.config}: SIR PMCMC, N={N} particles, pop=1e4, "
-                                   f"{T} obs, {C} independent chains per GPU",
+            "data": f"synthetic ({meta['describe']}); Philox-keyed filter draws",
+            "config": {"workload": f"BASELINE config {args.config}: {meta['model'].upper()} PMCMC, N={N} particles, "
+                                   f"pop={meta['n_population']}, {T} obs, {C} independent chains per GPU",
                        "particles": N, "T_obs": T, "chains_per_gpu": C, "population": meta["n_population"],
                        "parallelism": f"chains sharded over {world} GPU(s), RCCL all-gather of draws at end"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -55,8 +55,10 @@ int default_wg(int N) {
         int v = atoi(e);
         if (v == 64 || v == 256) return v;
     }
-    (void)N;
-    return 64;
+    // One wave per block keeps the in-block CDF short, but every block holds the 2B-double block-sum table in
+    // LDS: past ~16k particles (B > 256) that table caps occupancy (N = 5e4: 15 KB per 64-thread block, 2.5
+    // waves/SIMD), so large filters use 256-thread blocks (B = N/256).
+    return N > 16384 ? 256 : 64;
 }
 }  // namespace
 

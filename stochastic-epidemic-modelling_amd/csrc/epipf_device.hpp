@@ -491,60 +491,104 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
 }
 
 // The exact reference draw for every lane of the wave with need == true, all 64 lanes cooperating (call
-// from wave-uniform control flow; every lane must be active).  The weights are streamed in coalesced chunks
-// of 64; the sequential sums run on values broadcast with v_readlane, in the reference's order:
+// from wave-uniform control flow; every lane must be active).  The weights stream through the wave in
+// coalesced chunks of 64, kExactDepth chunks in flight (a single chunk ahead leaves each pass bound by one
+// L2/HBM round trip per chunk); the sequential sums run on values broadcast with v_readlane, in the
+// reference's order:
 //   pass 1  S = (((w_0 + w_1) + w_2) + ...)
 //   pass 2  last = c_{N-1},  c_i = c_{i-1} + w_i / S
-//   pass 3  first i with fl(c_i / last) > U, per needing lane (c_i / last via a certified product, with
-//           the IEEE division only within a few ulps of U); stops once every needing lane is resolved.
-// Cost ~3 x N dependent f64 adds for the wave (~0.1 ms at N = 10^4) instead of 3N dependent HBM loads.
-__device__ __noinline__ int resample_exact_wave(bool need, double U, const double* __restrict__ w, int N) {
-    const int lane = threadIdx.x & 63;
-    double S = 0.0;
-    double x = (lane < N) ? w[lane] : 0.0;
-    for (int base = 0; base < N; base += 64) {
-        const double xn = (base + 64 + lane < N) ? w[base + 64 + lane] : 0.0;   // prefetch the next chunk
-        if (base + 64 <= N) {
+//   pass 3  the needing lanes are served in increasing U: for the current target U*, the first i with
+//           fl(c_i / last) > U* (a certified product c_i * (1/last) decides, the IEEE division only within a
+//           few ulps of U*); the next target continues from the same i, since cdf is non-decreasing.  Every
+//           test in the loop is wave-uniform, and the pass stops at the last target.
+// Cost ~3 N dependent f64 adds for the wave.
+constexpr int kExactDepth = 4;
+
+struct ExactTarget {          // wave-uniform: smallest U among the lanes still waiting, or done
+    double U, lo, hi;
+    bool done;
+};
+
+__device__ __forceinline__ ExactTarget exact_next_target(bool waiting, double U) {
+    double m = waiting ? U : __builtin_inf();
 #pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmin(m, __shfl_xor(m, o, 64));
+    ExactTarget t;
+    t.U = m;
+    t.lo = m * (1.0 - 0x1.0p-49);     // |c * (1/last) - c / last| <= 2 ulp of c / last
+    t.hi = m * (1.0 + 0x1.0p-49);
+    t.done = !(m < __builtin_inf());
+    return t;
+}
+
+// rotating 4-deep prefetch of 64-element chunks (no indexed arrays, so nothing spills)
+struct ChunkStream {
+    const double* w;
+    int N, lane;
+    double x0, x1, x2, x3;
+    __device__ __forceinline__ double ld(int i) const { return (i < N) ? w[i] : 0.0; }
+    __device__ __forceinline__ void start(const double* w_, int N_) {
+        w = w_; N = N_; lane = threadIdx.x & 63;
+        x0 = ld(lane); x1 = ld(64 + lane); x2 = ld(128 + lane); x3 = ld(192 + lane);
+    }
+    __device__ __forceinline__ double next(int cb) {   // chunk at cb; issues the load of chunk cb + 256
+        const double x = x0;
+        x0 = x1; x1 = x2; x2 = x3;
+        x3 = ld(cb + 64 * kExactDepth + lane);
+        return x;
+    }
+};
+
+__device__ __forceinline__ int resample_exact_wave(bool need, double U, const double* __restrict__ w, int N) {
+    ChunkStream cs;
+    // pass 1: S
+    double S = 0.0;
+    cs.start(w, N);
+#pragma unroll 1
+    for (int cb = 0; cb < N; cb += 64) {
+        const double x = cs.next(cb);
+        if (cb + 64 <= N) {
+#pragma unroll 16
             for (int l = 0; l < 64; ++l) S = S + readlane_f64(x, l);
         } else {
-            for (int l = 0; l < N - base; ++l) S = S + readlane_f64(x, l);
+            for (int l = 0; l < N - cb; ++l) S = S + readlane_f64(x, l);
         }
-        x = xn;
     }
+    // pass 2: last = c_{N-1}
     double c = 0.0;
-    x = (lane < N) ? w[lane] : 0.0;
-    for (int base = 0; base < N; base += 64) {
-        const double xn = (base + 64 + lane < N) ? w[base + 64 + lane] : 0.0;
-        const double q = x / S;
-        if (base + 64 <= N) {
-#pragma unroll
+    cs.start(w, N);
+#pragma unroll 1
+    for (int cb = 0; cb < N; cb += 64) {
+        const double q = cs.next(cb) / S;
+        if (cb + 64 <= N) {
+#pragma unroll 16
             for (int l = 0; l < 64; ++l) c = c + readlane_f64(q, l);
         } else {
-            for (int l = 0; l < N - base; ++l) c = c + readlane_f64(q, l);
+            for (int l = 0; l < N - cb; ++l) c = c + readlane_f64(q, l);
         }
-        x = xn;
     }
     const double last = c;
     const double rl = 1.0 / last;
-    const double ulo = U * (1.0 - 0x1.0p-49), uhi = U * (1.0 + 0x1.0p-49);   // |c*rl - c/last| <= 2 ulp
+
+    // pass 3: serve the needing lanes in increasing U
     int ans = N - 1;
-    bool found = !need;
+    bool waiting = need;
+    ExactTarget tg = exact_next_target(waiting, U);
     c = 0.0;
-    x = (lane < N) ? w[lane] : 0.0;
-    for (int base = 0; base < N; base += 64) {
-        if (__all(found)) break;
-        const double xn = (base + 64 + lane < N) ? w[base + 64 + lane] : 0.0;
-        const double q = x / S;
-        const int n = min(64, N - base);
+    cs.start(w, N);
+#pragma unroll 1
+    for (int cb = 0; cb < N && !tg.done; cb += 64) {
+        const double q = cs.next(cb) / S;
+        const int n = min(64, N - cb);
         for (int l = 0; l < n; ++l) {
             c = c + readlane_f64(q, l);
             const double r = c * rl;
-            if (!found && r > ulo) {
-                if (r > uhi || c / last > U) { found = true; ans = base + l; }
+            while (!tg.done && r > tg.lo && (r > tg.hi || c / last > tg.U)) {   // cdf_i > U*: lanes at U* done
+                if (waiting && U == tg.U) { ans = cb + l; waiting = false; }
+                tg = exact_next_target(waiting, U);
             }
+            if (tg.done) break;
         }
-        x = xn;
     }
     return ans;
 }

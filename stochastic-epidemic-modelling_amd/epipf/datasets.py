@@ -81,25 +81,33 @@ def benchmark_dataset(cfg):
     """Observation matrices for the BASELINE.json configs.  Returns (Y, meta)."""
     if cfg == 1:
         ode = sir_simulate_discrete((180, 20, 0), np.linspace(0, 49, num=500), 2, 1)[:, 1:]
-        return thin_binomial(ode, 0.1, np.random.RandomState(2)), dict(model="sir", n_population=200, mu=20,
-                                                                        theta=(2.0, 1.0), probs=0.1)
+        return thin_binomial(ode, 0.1, np.random.RandomState(2)), dict(
+            model="sir", n_population=200, mu=20, theta=(2.0, 1.0), probs=0.1, N=100,
+            describe="ODE SIR y0=(180,20,0), beta=2, gamma=1, 50 daily rows, binomial thinning p=.1, RandomState(2)")
     if cfg == 2:
         ode = sir_simulate_discrete((9980, 20, 0), np.linspace(0, 199, num=2000), 0.25, 0.1)[:, 1:]
-        return thin_binomial(ode, 0.1, np.random.RandomState(1)), dict(model="sir", n_population=10000, mu=20,
-                                                                        theta=(0.25, 0.1), probs=0.1)
+        return thin_binomial(ode, 0.1, np.random.RandomState(1)), dict(
+            model="sir", n_population=10000, mu=20, theta=(0.25, 0.1), probs=0.1, N=10000,
+            describe="ODE SIR y0=(9980,20,0), beta=.25, gamma=.1, 200 daily rows, binomial thinning p=.1, "
+                     "RandomState(1)")
     if cfg == 3:
         ode = seir_simulate_discrete((9980, 0, 20, 0), np.linspace(0, 199, num=2000), 0.5, 0.2, 0.1)[:, 1:]
-        return noise_normal(ode, 0.1, np.random.RandomState(3)), dict(model="seir", n_population=10000, mu=20,
-                                                                       theta=(0.5, 0.2, 0.1), probs=0.1,
-                                                                       observations=True)
+        return noise_normal(ode, 0.1, np.random.RandomState(3)), dict(
+            model="seir", n_population=10000, mu=20, theta=(0.5, 0.2, 0.1), probs=0.1, observations=True, N=10000,
+            describe="ODE SEIR y0=(9980,0,20,0), beta=.5, alpha=.2, gamma=.1, 200 daily rows, Gaussian noise "
+                     "N(x, .1x) cast to int, RandomState(3); normal observation model")
     if cfg == 4:
         ode = sir_simulate_discrete((4800, 20, 0), np.linspace(0, 14, num=200), 2, 1)[:, 1:]
-        return thin_binomial(ode, 0.1, np.random.RandomState(11)), dict(model="sir", n_population=4820, mu=20,
-                                                                         theta=(2.0, 1.0), probs=0.1)
+        return thin_binomial(ode, 0.1, np.random.RandomState(11)), dict(
+            model="sir", n_population=4820, mu=20, theta=(2.0, 1.0), probs=0.1, N=50000,
+            describe="ODE SIR y0=(4800,20,0), beta=2, gamma=1, 15 daily rows, binomial thinning p=.1 "
+                     "(under-reported counts), RandomState(11)")
     if cfg == 5:
         pop = np.array([[2000, 30, 0], [3000, 40, 0]])
         ode = sir_subgroups_simulate_discrete(pop, np.linspace(0, 14, num=200), np.array([[5, 2], [1, 3]]), 0.5)
         return thin_binomial(ode[:, :6], 0.1, np.random.RandomState(14)), dict(
             model="sir_subgroups", n_population=[2030, 3040], mu=[30, 40], theta=[4.0, 1.0, 1.0, 4.0, 1.0],
-            probs=0.1)
+            probs=0.1, N=10000,
+            describe="ODE 2-group SIR pop=[[2000,30,0],[3000,40,0]], beta=[[5,2],[1,3]], gamma=.5, 15 daily rows, "
+                     "binomial thinning p=.1, RandomState(14)")
     raise ValueError(f"unknown benchmark config {cfg}")
