@@ -69,6 +69,7 @@ struct epipf_ctx {
     int32_t *hidden = nullptr, *ancestry = nullptr, *status = nullptr, *chosen = nullptr, *traj = nullptr;
     double *wraw = nullptr, *wloc = nullptr, *bsum = nullptr, *log_zeta = nullptr, *Y = nullptr, *lf = nullptr;
     ChainParam* cp = nullptr;
+    LogTab* logtab = nullptr;
     unsigned long long* counters = nullptr;
     // pinned staging
     ChainParam* h_cp = nullptr;
@@ -103,7 +104,7 @@ static void free_ctx(epipf_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* dev[] = {c->hidden, c->ancestry, c->status, c->chosen, c->traj, c->wraw, c->wloc, c->bsum,
-                   c->log_zeta, c->Y, c->lf, c->cp, c->counters, c->scratch};
+                   c->log_zeta, c->Y, c->lf, c->cp, c->logtab, c->counters, c->scratch};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     void* host[] = {c->h_cp, c->h_status, c->h_lz, c->h_counters};
@@ -170,6 +171,7 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     rc |= dalloc(&c->bsum, 2 * (size_t)max_chains * c->bstride);
     rc |= dalloc(&c->log_zeta, (size_t)max_chains * t_max);
     rc |= dalloc(&c->cp, (size_t)max_chains);
+    rc |= dalloc(&c->logtab, (size_t)kLogTabEntries);
     rc |= dalloc(&c->counters, (size_t)kCounterSlots * kCounterStride);
     if (rc) { free_ctx(c); return EPIPF_ENOMEM; }
     if (hipHostMalloc((void**)&c->h_cp, sizeof(ChainParam) * max_chains) != hipSuccess ||
@@ -181,7 +183,8 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     }
     for (auto& e : c->ev)
         if (hipEventCreate(&e) != hipSuccess) { free_ctx(c); return fail(EPIPF_EHIP, "hipEventCreate failed"); }
-    if (hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride, c->stream) != hipSuccess ||
+    if (launch_log_table(c->logtab, c->stream) != hipSuccess ||
+        hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
         free_ctx(c);
         return fail(EPIPF_EHIP, "counter init failed");
@@ -278,7 +281,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     a.resample_mode = resample_mode; a.count_events = c->profiling >= EPIPF_PROFILE_COUNTERS ? 1 : 0; a.lf_max = c->lf_max;
     a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride; a.wstride = c->wstride; a.bstride = c->bstride;
     a.cert_k = cert_k(c->N, c->B, c->wg);
-    a.Y = c->Y; a.lf = c->lf; a.cp = c->cp; a.hidden = c->hidden; a.ancestry = c->ancestry;
+    a.Y = c->Y; a.lf = c->lf; a.logtab = c->logtab; a.cp = c->cp; a.hidden = c->hidden; a.ancestry = c->ancestry;
     a.wraw = c->wraw; a.wloc = c->wloc; a.bsum = c->bsum; a.log_zeta = c->log_zeta; a.status = c->status;
     a.counters = c->counters;
     for (int g = 0; g < kMaxG; ++g) { a.npop[g] = c->npop[g]; a.mu[g] = c->mu[g]; a.emu[g] = c->emu[g]; a.kmax[g] = c->kmax[g]; }
@@ -405,7 +408,7 @@ int epipf_simulate(epipf_ctx* c, int n, const int32_t* states_in, const double* 
     HIP_TRY(hipMemcpyAsync(din, states_in, sizeof(int32_t) * (size_t)n * c->C, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(dev_events, 0, sizeof(unsigned long long), c->stream));
     SimArgs a{};
-    a.n = n; a.step = step; a.tmax = max_time; a.cp = dcp; a.in = din; a.out = dout; a.events = dev_events;
+    a.logtab = c->logtab; a.n = n; a.step = step; a.tmax = max_time; a.cp = dcp; a.in = din; a.out = dout; a.events = dev_events;
     hipError_t le = launch_simulate(a, c->model, c->G, c->stream);
     if (le != hipSuccess) return fail(EPIPF_EHIP, "simulate launch failed: %s", hipGetErrorString(le));
     unsigned long long ev = 0;

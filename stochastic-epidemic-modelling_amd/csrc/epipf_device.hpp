@@ -348,8 +348,9 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
     double t = 0.0;
     uint32_t k = 0;
     int nev = 0;
-    Block rn = philox(0u, j, ptag, cp.f, cp.k0, cp.k1);
     bool alive = st.active();
+    Block rn{0u, 0u, 0u, 0u};
+    if (alive) rn = philox(0u, j, ptag, cp.f, cp.k0, cp.k1);
     while (alive) {
         const Block r = rn;                                            // this event's block
         ++k;
@@ -395,7 +396,23 @@ __device__ __forceinline__ double normal_pdf(double y, double x, double probs) {
     return (exp(-(z * z) / 2.0) / 2.5066282746310002) / scale;
 }
 
-// min over the K observed columns (np.min propagates NaN)
+// log of binom_pmf with the same expression order: -inf for pmf 0, 0 for pmf 1, NaN for bad p
+__device__ __forceinline__ double binom_logpmf(double k, double n, const ChainParam& cp, const double* lf, int lf_max) {
+    const double p = cp.probs;
+    if (!(p >= 0.0 && p <= 1.0)) return __builtin_nan("");
+    if (k < 0.0 || k > n || k != floor(k)) return -__builtin_inf();
+    if (p == 0.0) return (k == 0.0) ? 0.0 : -__builtin_inf();
+    if (p == 1.0) return (k == n) ? 0.0 : -__builtin_inf();
+    const int ni = min(max((int)n, 0), lf_max), ki = min(max((int)k, 0), lf_max);
+    double a = lf[ni] - lf[ki];
+    a = a - lf[min(max(ni - ki, 0), lf_max)];
+    const double b = k * cp.logp;
+    const double c = (n - k) * cp.log1mp;
+    return a + (b + c);
+}
+
+// min over the K observed columns (np.min propagates NaN), pmcmc.py:178-181.  Binomial: exp is monotone, so
+// min_i exp(L_i) = exp(min_i L_i) -- one exp per particle instead of K, same value.
 template <int MODEL, int G, int OBS>
 __device__ __forceinline__ double particle_weight(const double* x, const double* yrow, const ChainParam& cp,
                                                   const double* lf, int lf_max) {
@@ -411,11 +428,11 @@ __device__ __forceinline__ double particle_weight(const double* x, const double*
         } else {
             xo = x[i];
         }
-        const double wi = (OBS == kBinomial) ? binom_pmf(yrow[i], xo, cp, lf, lf_max) : normal_pdf(yrow[i], xo, cp.probs);
+        const double wi = (OBS == kBinomial) ? binom_logpmf(yrow[i], xo, cp, lf, lf_max) : normal_pdf(yrow[i], xo, cp.probs);
         if (i == 0 || isnan(wi)) w = wi;
         else if (!isnan(w) && wi < w) w = wi;
     }
-    return w;
+    return (OBS == kBinomial) ? exp(w) : w;
 }
 
 // ------------------------------------------------------------------------------- block scan (doubles)

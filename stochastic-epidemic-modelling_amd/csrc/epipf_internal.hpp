@@ -31,6 +31,7 @@ struct StepArgs {
     double cert_k;                // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp)
     const double* Y;
     const double* lf;
+    const LogTab* logtab;         // fast_log table [kLogTabEntries] (context-resident)
     const ChainParam* cp;
     int32_t* hidden;
     int32_t* ancestry;
@@ -55,6 +56,7 @@ struct PathArgs {
 };
 
 struct SimArgs {
+    const LogTab* logtab;
     int n;
     uint32_t step;
     double tmax;
@@ -81,6 +83,7 @@ size_t step_lds_bytes(int B, int wg);
 hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, hipStream_t s,
                          hipEvent_t ev_init, hipEvent_t ev_step0, hipEvent_t ev_end);
 hipError_t launch_path_sample(const PathArgs& a, hipStream_t s);
+hipError_t launch_log_table(LogTab* tab, hipStream_t s);
 hipError_t launch_simulate(const SimArgs& a, int model, int G, hipStream_t s);
 hipError_t launch_resample(const ResampleArgs& a, hipStream_t s);
 

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
     const int tid = threadIdx.x;
     const int j = blockIdx.x * WG + tid;
     if (a.status[chain] != 0) return;
-    for (int i = tid; i < kLogTabEntries; i += WG) log_table_entry(tab, i);   // published by the barriers below
+    for (int i = tid; i < kLogTabEntries; i += WG) tab[i] = a.logtab[i];    // published by the barriers below
     const ChainParam cp = a.cp[chain];
     const int prev = (p - 1) & 1, cur = p & 1;
     const size_t wprev = ((size_t)prev * a.max_chains + chain) * a.wstride;
@@ -182,6 +182,9 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
     }
 }
 
+// the fast_log table, built once per context on the device (so it uses the device log)
+__global__ void log_table_kernel(LogTab* tab) { log_table_entry(tab, threadIdx.x); }
+
 // particle_path_sampler, pmcmc.py:236-248 (one lane per chain; T dependent loads)
 __global__ void path_sample_kernel(PathArgs a) {
     const int chain = blockIdx.x * blockDim.x + threadIdx.x;
@@ -201,7 +204,7 @@ template <int MODEL, int G>
 __global__ __launch_bounds__(256) void simulate_kernel(SimArgs a) {
     constexpr int C = Shape<MODEL, G>::C;
     __shared__ LogTab tab[kLogTabEntries];
-    if (threadIdx.x < kLogTabEntries) log_table_entry(tab, threadIdx.x);
+    if (threadIdx.x < kLogTabEntries) tab[threadIdx.x] = a.logtab[threadIdx.x];
     __syncthreads();
     const int j = blockIdx.x * 256 + threadIdx.x;
     int nev = 0, iters = 0;
@@ -312,6 +315,11 @@ hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_cha
                          hipEvent_t ev_init, hipEvent_t ev_step0, hipEvent_t ev_end) {
     if (a.wg == 64) return launch_model<64>(a, model, G, obs, n_chains, s, ev_init, ev_step0, ev_end);
     return launch_model<256>(a, model, G, obs, n_chains, s, ev_init, ev_step0, ev_end);
+}
+
+hipError_t launch_log_table(LogTab* tab, hipStream_t s) {
+    hipLaunchKernelGGL(log_table_kernel, dim3(1), dim3(kLogTabEntries), 0, s, tab);
+    return hipGetLastError();
 }
 
 hipError_t launch_path_sample(const PathArgs& a, hipStream_t s) {
