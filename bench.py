@@ -86,12 +86,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("EPIPF_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI; gloo only for rehearsals
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
+        ndev = torch.cuda.device_count()
+        local = local % max(ndev, 1)      # one GPU per rank on a full node; ranks share GPUs in rehearsals
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     import torch
 
     from epipf import datasets
@@ -139,7 +142,8 @@ def main():
 
     # max over ranks of the wall time; sum of filters
     if dist is not None:
-        tt = torch.tensor([dt, float(filters)], dtype=torch.float64, device=f"cuda:{local}")
+        tt = torch.tensor([dt, float(filters)], dtype=torch.float64,
+                          device=f"cuda:{local}" if backend == "nccl" else "cpu")
         mx = tt.clone()
         dist.all_reduce(mx[0:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(mx[1:2], op=dist.ReduceOp.SUM)
