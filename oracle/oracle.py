@@ -19,7 +19,8 @@ MODEL_IDS = {"sir": 0, "seir": 1, "sir_subgroups": 2, "sir_subgroups2": 3}
 
 def build(force=False):
     if force or not os.path.exists(_LIB_PATH) or (
-        os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "epipf_oracle.c"))
+        os.path.getmtime(_LIB_PATH) < max(os.path.getmtime(os.path.join(_HERE, f))
+                                          for f in ("epipf_oracle.c", "abc_oracle.c", "Makefile"))
     ):
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
@@ -45,6 +46,14 @@ def lib():
         L.oracle_binom_pmf.restype = f64
         L.oracle_norm_pdf.argtypes = [f64, f64, f64]
         L.oracle_norm_pdf.restype = f64
+        L.oracle_abc_trials.argtypes = [P, i32, P, P, P, u64, u32, u32, i32, P, P, P, P]
+        L.oracle_abc_trials.restype = i32
+        L.oracle_pairwise_sum.argtypes = [P, ctypes.c_long]
+        L.oracle_pairwise_sum.restype = f64
+        L.oracle_poisson_mode_pmf.argtypes = [f64]
+        L.oracle_poisson_mode_pmf.restype = f64
+        L.oracle_poisson_mode_inversion.argtypes = [f64, f64, f64]
+        L.oracle_poisson_mode_inversion.restype = ctypes.c_long
         _lib = L
     return _lib
 
@@ -134,3 +143,52 @@ def norm_pdf(y, x, probs):
 
 def num_threads():
     return lib().oracle_num_threads()
+
+
+# ----------------------------------------------------------------------------------- ABC (abc_algo.py:17-109)
+def abc_start(observed_data):
+    """Initial-count means (abc_algo.py:38 Y[0].astype(int)) and their mode probabilities."""
+    Y = np.asarray(observed_data, dtype=np.float64)
+    lams = Y[0, :3].astype(int).astype(np.float64)
+    if (lams < 0).any():
+        raise ValueError("lam < 0")
+    pms = np.array([lib().oracle_poisson_mode_pmf(v) if v > 0 else 0.0 for v in lams])
+    return lams, pms
+
+
+def abc_trials(observed_data, priors, key=0, run_index=0, t0=0, n=1, rows=True):
+    """Trials [t0, t0+n): theta [n,2], rows [n,T,3] int32 (S, I, R per day) or None, distance [n], events."""
+    Y = np.ascontiguousarray(np.asarray(observed_data, dtype=np.float64)[:, :3])
+    T = Y.shape[0]
+    pr = np.ascontiguousarray(np.array(list(priors["beta"]) + list(priors["gamma"]), dtype=np.float64))
+    lams, pms = abc_start(Y)
+    theta = np.zeros((n, 2))
+    rw = np.zeros((n, T, 3), dtype=np.int32) if rows else None
+    dist = np.zeros(n)
+    ev = np.zeros(1, dtype=np.int64)
+    st = lib().oracle_abc_trials(_p(Y), T, _p(pr), _p(lams), _p(pms), int(key) & (2**64 - 1),
+                                 int(run_index) & 0xFFFFFFFF, int(t0), int(n), _p(theta),
+                                 _p(rw) if rows else None, _p(dist), _p(ev))
+    if st < 0:
+        raise ValueError("oracle_abc_trials: bad arguments")
+    return theta, rw, dist, int(ev[0])
+
+
+def abc_algo(observed_data, no_of_samples, threshold, priors, key=0, run_index=0, batch=4096, max_trials=10**9):
+    """abc_algo.abc_algo on the keyed stream: (posterior dict, trajectories [n,T,4] float64, trials)."""
+    T = np.asarray(observed_data).shape[0]
+    betas, gammas, trajs = [], [], []
+    t = 0
+    while len(betas) < no_of_samples and t < max_trials:
+        n = min(batch, max_trials - t)
+        theta, rw, dist, _ = abc_trials(observed_data, priors, key, run_index, t, n)
+        for i in np.nonzero(~(dist > threshold))[0]:
+            if len(betas) == no_of_samples:
+                break
+            betas.append(float(theta[i, 0]))
+            gammas.append(float(theta[i, 1]))
+            trajs.append(np.concatenate([np.arange(T, dtype=np.float64)[:, None], rw[i].astype(np.float64)], 1))
+            last = t + int(i)
+        t += n
+    trials = last + 1 if betas else t
+    return {"beta": betas, "gamma": gammas}, np.array(trajs).reshape(-1, T, 4), trials

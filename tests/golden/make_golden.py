@@ -55,6 +55,9 @@ class _Stream:
     k = 0
     u2 = None
     direct = False  # direct SSA call: (p, j) set by the caller
+    abc = False     # abc_algo run: uniforms / poisson / SSA draws come from the ABC domains
+    abc_uniforms = 0
+    t = 0
 
 
 S = _Stream()
@@ -82,7 +85,10 @@ class _RandomProxy:
 
     def exponential(self, scale=1.0, size=None):
         assert size is None
-        u1, u2 = ph.ssa_uniforms(S.key, S.f, S.p, S.j, S.k)
+        if S.abc:
+            u1, u2 = ph.abc_ssa_uniforms(S.key, S.f, S.t, S.k)
+        else:
+            u1, u2 = ph.ssa_uniforms(S.key, S.f, S.p, S.j, S.k)
         S.k += 1
         S.u2 = float(u2)
         return scale * (-math.log(1.0 - float(u1)))
@@ -97,7 +103,21 @@ class _RandomProxy:
         _INJ.u = ph.resample_uniforms(S.key, S.f, S.resamples, int(size))
         return _INJ.choice(a, size, replace, p)
 
+    def uniform(self, low=0.0, high=1.0, size=None):
+        assert S.abc and size is None
+        c = S.abc_uniforms
+        S.abc_uniforms += 1
+        S.t = c // 2  # abc_algo.py:35-36: beta then gamma, one trial per pair
+        return low + (high - low) * ph.abc_prior_uniforms(S.key, S.f, S.t)[c % 2]
+
     def poisson(self, lam=1.0, size=None):
+        if S.abc:  # abc_algo.py:39 np.random.poisson(n_start), n_start an int array
+            lam = np.asarray(lam)
+            assert size is None and lam.dtype.kind == "i"
+            lams = [float(v) for v in lam]
+            return np.array(ph.abc_initial_counts(S.key, S.f, S.t, lams,
+                                                  [ph.poisson_mode_pmf(v) if v > 0 else 0.0 for v in lams]),
+                            dtype=lam.dtype)
         g = S.poissons
         S.poissons += 1
         u = ph.init_uniforms(S.key, S.f, g, int(size))
@@ -308,6 +328,45 @@ def run_ssa_cases(pm, ga, out):
                 step=3, out=np.array(res).astype(np.int32), model=name.split("_")[0])
 
 
+ABC_CASES = [
+    # name, dataset, row0 override (S, I, R) or None, no_of_samples, threshold, priors, key
+    # (abc_algo.py's daily-table assembly is quadratic in the event count: a trial costs ~0.2-0.6 s, so the
+    # thresholds are set for a few percent acceptance and a few accepted samples)
+    ("noisy_400", "sir_noisy", None, 3, 400.0, {"beta": [0, 5], "gamma": [0, 5]}, 3001),
+    ("noisy_150", "sir_noisy", None, 3, 150.0, {"beta": [1.0, 3.0], "gamma": [0.5, 1.5]}, 3002),
+    ("extinct_all", "sir_noisy", (4815, 3, 2), 16, 1e9, {"beta": [0, 3], "gamma": [0, 3]}, 3003),
+    ("float_obs_15", "sir_ode", None, 3, 120.0, {"beta": [1.0, 3.0], "gamma": [0.5, 1.5]}, 3004),
+    ("float_obs_200", "cfg2_ode/50", (180, 20, 0), 6, 1e9, {"beta": [0.2, 0.3], "gamma": [0.05, 0.15]}, 3005),
+]
+
+
+def run_abc_cases(ab, d, out):
+    """abc_algo.abc_algo (abc_algo.py:17-109) run unmodified on the keyed ABC stream."""
+    orig = ab.sir_simulate
+
+    def ssa(*a, **k):
+        S.k = 0
+        S.u2 = None
+        return orig(*a, **k)
+
+    ab.sir_simulate = ssa
+    for name, ds, row0, n, thr, priors, key in ABC_CASES:
+        Y = d[ds].copy() if "/" not in ds else d[ds.split("/")[0]] / float(ds.split("/")[1])
+        if row0 is not None:
+            Y[0] = row0
+        S.abc, S.key, S.f, S.abc_uniforms = True, key, 0, 0
+        t0 = time.time()
+        post, trajs = ab.abc_algo(Y, n, thr, priors)
+        dt = time.time() - t0
+        S.abc = False
+        out["abc_" + name] = dict(Y=Y, n=n, threshold=thr, priors=np.array(priors["beta"] + priors["gamma"], float),
+                                  key=key, f=0, beta=np.array(post["beta"]), gamma=np.array(post["gamma"]),
+                                  trajectories=np.asarray(trajs, dtype=np.float64), trials=S.abc_uniforms // 2,
+                                  seconds=dt)
+        print(f"abc {name}: trials={S.abc_uniforms // 2} {dt:.1f}s", flush=True)
+    ab.sir_simulate = orig
+
+
 def run_resample_cases(out):
     rs = np.random.RandomState(31)
     for n in (1, 2, 5, 64, 257, 1000):
@@ -389,11 +448,13 @@ def main():
     matplotlib.use("Agg")
     import gillespie_algo as ga
     import pmcmc as pm
+    import abc_algo as ab
 
     check_numpy_identities()
     d = make_datasets(pm)
     np.savez_compressed(os.path.join(HERE, "datasets.npz"), **d)
     pf = install_shim(pm, ga)
+    ab.np = pm.np
     only = set(args.only.split(",")) if args.only else None
     if not only or "filter" in only:
         out = {}
@@ -409,6 +470,10 @@ def main():
         out = {}
         run_pmcmc_cases(pm, d, out)
         save(out, os.path.join(HERE, "pmcmc_golden.npz"))
+    if not only or "abc" in only:
+        out = {}
+        run_abc_cases(ab, d, out)
+        save(out, os.path.join(HERE, "abc_golden.npz"))
 
 
 if __name__ == "__main__":
