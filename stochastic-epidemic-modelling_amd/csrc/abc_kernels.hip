@@ -1,0 +1,174 @@
+// abc_kernels.hip -- ABC rejection sampling (abc_algo.py:17-109) on MI355X.
+//
+// abc_trials_kernel  one lane per trial t: prior draw (:35-36), initial counts (:38-39), the full SIR path
+//                    (:40-45 -> gillespie_algo.py:10-75) recorded straight into the daily table the reference
+//                    assembles afterwards (:47-88).
+// abc_distance_kernel the distance (:89-94) with numpy's pairwise mean, one lane per trial.
+// abc_select_kernel  the first `need` trials with !(distance > threshold), in trial order (:30-33 -- the
+//                    reference's while loop accepts trials in exactly that order).
+// abc_gather_kernel  accepted thetas and [T][4] trajectories (day, S, I, R) into the output slots.
+//
+// The day table needs no event history: day d holds the state after every event with time <= d (ceil(time)
+// groups events into day rows, missing days repeat the previous row), so a lane writes day rows as its clock
+// passes integer days.  An event past day T-1 only changes row T, which :88 truncates away: the walk stops.
+#include "abc_device.hpp"
+#include "epipf_internal.hpp"
+
+namespace epipf {
+
+__device__ __forceinline__ void write_day(int32_t* col, size_t n, int d, double S, double I, double R) {
+    int32_t* p = col + (size_t)d * 3 * n;
+    p[0] = (int32_t)S;
+    p[n] = (int32_t)I;
+    p[2 * n] = (int32_t)R;
+}
+
+__global__ __launch_bounds__(256) void abc_trials_kernel(AbcArgs a) {
+    __shared__ LogTab tab[kLogTabEntries];
+    if (threadIdx.x < kLogTabEntries) tab[threadIdx.x] = a.logtab[threadIdx.x];
+    __syncthreads();
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    int nev = 0, iters = 0;
+    if (i < a.n) {
+        const uint32_t t = a.t0 + (uint32_t)i;
+        const size_t n = (size_t)a.n;
+        ChainParam cp;
+        const Block rp = philox(0u, t, kDomainAbcPrior, a.f, a.k0, a.k1);
+        cp.theta[0] = a.prior_lo[0] + a.prior_rng[0] * u01(rp.x, rp.y);         // abc_algo.py:35
+        cp.theta[1] = a.prior_lo[1] + a.prior_rng[1] * u01(rp.z, rp.w);         // :36
+        double x[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {                                           // :38-39
+            const Block r = philox((uint32_t)c, t, kDomainAbcInit, a.f, a.k0, a.k1);
+            x[c] = (double)poisson_mode_inversion(a.lam[c], u01(r.x, r.y), a.pm[c]);
+        }
+        SsaState<kSIR, 1> st;
+        st.load(x, cp);
+        const double R0 = x[2];
+        const double last_day = (double)(a.T - 1);
+        int32_t* col = a.days + i;
+        double clock = 0.0, next_day = 0.0;
+        int day = 0;
+        uint32_t k = 0;
+        bool alive = st.active();
+        Block rn{0u, 0u, 0u, 0u};
+        if (alive) rn = philox(0u, t, kDomainAbcSsa, a.f, a.k0, a.k1);
+        while (alive) {                          // every lane enters at k = 0: k stays wave-uniform
+            const Block r = rn;
+            ++k;
+            rn = philox(__builtin_amdgcn_readfirstlane(k), t, kDomainAbcSsa, a.f, a.k0, a.k1);
+            const double S0 = st.S, I0 = st.I;
+            const int rec0 = st.nrec;
+            const bool ev = st.event(r, clock, last_day, cp, tab);   // false: the event lands after day T-1
+            if (ev) {
+                ++nev;
+                while (next_day < clock) {                               // days the event does not reach
+                    write_day(col, n, day, S0, I0, R0 + (double)rec0);
+                    ++day;
+                    next_day += 1.0;
+                }
+            }
+            alive = ev && st.active();
+        }
+        for (; day < a.T; ++day) write_day(col, n, day, st.S, st.I, R0 + (double)st.nrec);
+        iters = (int)k;
+        a.theta[i] = cp.theta[0];
+        a.theta[n + i] = cp.theta[1];
+    }
+    if (a.count) {
+        unsigned long long e = (unsigned long long)nev, li = (unsigned long long)iters;
+        int wmax = iters;
+        for (int o = 32; o > 0; o >>= 1) {
+            e += __shfl_xor(e, o, 64);
+            li += __shfl_xor(li, o, 64);
+            wmax = max(wmax, __shfl_xor(wmax, o, 64));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            unsigned long long* slot = counter_slot(a.counters);
+            atomicAdd(slot, e);
+            atomicAdd(slot + 2, li);
+            atomicAdd(slot + 3, 64ull * (unsigned long long)wmax);
+        }
+    }
+}
+
+// distance_function (abc_algo.py:9-13, :89-94) of each trial's day table; a kernel of its own so the numpy
+// pairwise recursion (function calls, stack) stays out of the SSA kernel's register budget.
+// T <= 128 (one pairwise block) instantiates without any call.
+template <bool DEEP>
+__global__ __launch_bounds__(256) void abc_distance_kernel(AbcArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    const size_t n = (size_t)a.n;
+    const int32_t* col = a.days + i;
+    const AbsDiff vi{col + n, 3 * n, a.Y + 1}, vr{col + 2 * n, 3 * n, a.Y + 2};
+    const double dT = (double)a.T;
+    const double si = DEEP ? pairwise_sum<kAbcPairwiseDepth>(vi, 0, a.T) : pairwise_leaf(vi, 0, a.T);
+    const double sr = DEEP ? pairwise_sum<kAbcPairwiseDepth>(vr, 0, a.T) : pairwise_leaf(vr, 0, a.T);
+    a.dist[i] = (si / dT + sr / dT) / 2.0;
+}
+
+// One workgroup walks the batch in 1024-trial chunks: ballot + per-wave popcounts give each accepted trial its
+// rank; the walk ends once `need` trials are found.
+__global__ __launch_bounds__(1024) void abc_select_kernel(AbcSelectArgs a) {
+    __shared__ int wsum[16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int base = 0;
+    for (int c0 = 0; c0 < a.n && base < a.need; c0 += 1024) {
+        const int i = c0 + (int)threadIdx.x;
+        const bool acc = i < a.n && !(a.dist[i] > a.threshold);                // :30-33
+        const unsigned long long m = __ballot(acc);
+        if (lane == 0) wsum[w] = __popcll(m);
+        __syncthreads();
+        int off = 0, tot = 0;
+        for (int q = 0; q < 16; ++q) {
+            off += q < w ? wsum[q] : 0;
+            tot += wsum[q];
+        }
+        const int pos = base + off + __popcll(m & ((1ull << lane) - 1ull));
+        if (acc && pos < a.need) a.idx[pos] = i;
+        base += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *a.count = min(base, a.need);
+}
+
+__global__ __launch_bounds__(256) void abc_gather_kernel(AbcGatherArgs a, int max_count) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    const int s = g / a.T, d = g % a.T;
+    if (s >= max_count || s >= *a.count) return;
+    const size_t n = (size_t)a.n;
+    const int i = a.idx[s];
+    const int32_t* p = a.days + (size_t)d * 3 * n + i;
+    double* o = a.traj + ((size_t)(a.slot0 + s) * a.T + d) * 4;
+    o[0] = (double)d;                                                          // np.ceil(time) column
+    o[1] = (double)p[0];
+    o[2] = (double)p[n];
+    o[3] = (double)p[2 * n];
+    if (d == 0) {
+        a.theta_out[(size_t)(a.slot0 + s) * 2] = a.theta[i];
+        a.theta_out[(size_t)(a.slot0 + s) * 2 + 1] = a.theta[n + i];
+    }
+}
+
+hipError_t launch_abc_trials(const AbcArgs& a, hipStream_t s) {
+    if (a.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(abc_trials_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    if (a.T <= 128) hipLaunchKernelGGL(abc_distance_kernel<false>, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(abc_distance_kernel<true>, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_abc_select(const AbcSelectArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(abc_select_kernel, dim3(1), dim3(1024), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_abc_gather(const AbcGatherArgs& a, int max_count, hipStream_t s) {
+    if (max_count <= 0) return hipSuccess;
+    const long total = (long)max_count * a.T;
+    hipLaunchKernelGGL(abc_gather_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a, max_count);
+    return hipGetLastError();
+}
+
+}  // namespace epipf

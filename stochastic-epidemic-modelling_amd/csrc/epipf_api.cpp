@@ -6,6 +6,7 @@
 // chain) and the log-likelihoods + status (device->host) over PCIe.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -15,6 +16,7 @@
 #include <vector>
 
 #include "../../include/epipf.h"
+#include "abc_device.hpp"
 #include "epipf_internal.hpp"
 
 using namespace epipf;
@@ -86,6 +88,9 @@ struct epipf_ctx {
     // scratch for epipf_simulate / epipf_resample (grown on demand)
     size_t scratch_bytes = 0;
     void* scratch = nullptr;
+    // ABC buffers (grown on demand): days, theta, dist for one batch; Y; accepted idx/count; output slots
+    size_t abc_bytes = 0;
+    void* abc = nullptr;
 };
 
 // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp): D bounds the depth of the parallel
@@ -104,7 +109,7 @@ static void free_ctx(epipf_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* dev[] = {c->hidden, c->ancestry, c->status, c->chosen, c->traj, c->wraw, c->wloc, c->bsum,
-                   c->log_zeta, c->Y, c->lf, c->cp, c->logtab, c->counters, c->scratch};
+                   c->log_zeta, c->Y, c->lf, c->cp, c->logtab, c->counters, c->scratch, c->abc};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     void* host[] = {c->h_cp, c->h_status, c->h_lz, c->h_counters};
@@ -455,6 +460,219 @@ int epipf_resample(epipf_ctx* c, int n, const double* w, const double* u, int32_
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (fallbacks_out) *fallbacks_out = (int64_t)fb;
     return st ? EPIPF_STATUS_DEGENERATE : EPIPF_OK;
+}
+
+// ------------------------------------------------------------------------------- ABC rejection
+namespace {
+struct AbcPlan {
+    AbcArgs args{};
+    double* Ydev = nullptr;
+    int32_t* idx = nullptr;
+    int32_t* count = nullptr;
+    double* traj = nullptr;
+    double* theta_out = nullptr;
+};
+
+// Validates the reference-level arguments and fills the launch constants (abc_algo.py:35-39).
+int abc_prepare(epipf_ctx* c, const double* Y, int T, const double* priors, uint64_t key, uint32_t run_index,
+                AbcArgs& a) {
+    if (!c || !Y || !priors) return fail(EPIPF_EINVAL, "NULL argument");
+    if (T < 1 || T > kAbcMaxDays) return fail(EPIPF_EINVAL, "T=%d outside [1, %d]", T, kAbcMaxDays);
+    for (int q = 0; q < 4; ++q)
+        if (!(priors[q] >= 0.0 && priors[q] < INFINITY))
+            return fail(EPIPF_EINVAL, "priors[%d]=%g: prior bounds must be finite and >= 0", q, priors[q]);
+    for (int q = 0; q < 3 * T; ++q)
+        if (!std::isfinite(Y[q])) return fail(EPIPF_EINVAL, "observed_data[%d][%d] is not finite", q / 3, q % 3);
+    memset(&a, 0, sizeof a);
+    for (int j = 0; j < 2; ++j) {
+        a.prior_lo[j] = priors[2 * j];
+        a.prior_rng[j] = priors[2 * j + 1] - priors[2 * j];           // numpy uniform: low + (high - low) * U
+    }
+    for (int q = 0; q < 3; ++q) {
+        const double lam = std::trunc(Y[q]);                           // Y[0].astype(int), :38
+        if (lam < 0.0) return fail(EPIPF_EINVAL, "observed_data[0][%d]=%g: Poisson lam < 0 (numpy raises)", q, Y[q]);
+        if (lam > 1e9) return fail(EPIPF_EINVAL, "observed_data[0][%d]=%g: initial count above 1e9", q, Y[q]);
+        a.lam[q] = lam;
+        a.pm[q] = lam > 0.0 ? std::exp(-lam + lam * std::log(lam) - std::lgamma(lam + 1.0)) : 0.0;   // host glibc
+    }
+    a.T = T;
+    a.f = run_index;
+    a.k0 = (uint32_t)key;
+    a.k1 = (uint32_t)(key >> 32);
+    a.logtab = c->logtab;
+    a.counters = c->counters;
+    a.count = c->profiling >= EPIPF_PROFILE_COUNTERS ? 1 : 0;
+    return 0;
+}
+
+// Carves the ABC buffers for batches of up to `batch` trials and `samples` output slots.
+int abc_buffers(epipf_ctx* c, int T, int batch, int samples, AbcPlan& p) {
+    const size_t b = (size_t)batch;
+    const size_t sz_days = align256(sizeof(int32_t) * 3 * (size_t)T * b), sz_theta = align256(sizeof(double) * 2 * b),
+                 sz_dist = align256(sizeof(double) * b), sz_Y = align256(sizeof(double) * 3 * (size_t)T),
+                 sz_idx = align256(sizeof(int32_t) * (size_t)(samples + 1)), sz_cnt = 256,
+                 sz_traj = align256(sizeof(double) * 4 * (size_t)T * samples), sz_to = align256(sizeof(double) * 2 * (size_t)samples);
+    const size_t need = sz_days + sz_theta + sz_dist + sz_Y + sz_idx + sz_cnt + sz_traj + sz_to;
+    if (need > c->abc_bytes) {
+        if (c->abc) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->abc); c->abc = nullptr; c->abc_bytes = 0; }
+        if (hipMalloc(&c->abc, need) != hipSuccess) return fail(EPIPF_ENOMEM, "ABC buffers hipMalloc(%zu) failed", need);
+        c->abc_bytes = need;
+    }
+    char* q = (char*)c->abc;
+    p.args.days = (int32_t*)q; q += sz_days;
+    p.args.theta = (double*)q; q += sz_theta;
+    p.args.dist = (double*)q; q += sz_dist;
+    p.Ydev = (double*)q; q += sz_Y;
+    p.idx = (int32_t*)q; q += sz_idx;
+    p.count = (int32_t*)q; q += sz_cnt;
+    p.traj = (double*)q; q += sz_traj;
+    p.theta_out = (double*)q;
+    p.args.Y = p.Ydev;
+    return 0;
+}
+
+int abc_launch_trials(epipf_ctx* c, AbcArgs& a, uint32_t t0, int n) {
+    a.t0 = t0;
+    a.n = n;
+    if (c->profiling) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+    hipError_t le = launch_abc_trials(a, c->stream);
+    if (le != hipSuccess) return fail(EPIPF_EHIP, "ABC trial kernel launch failed: %s", hipGetErrorString(le));
+    if (c->profiling) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    return 0;
+}
+
+int abc_account(epipf_ctx* c, int n) {
+    if (c->profiling) {
+        HIP_TRY(hipEventSynchronize(c->ev[1]));
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+        c->stats.abc_ms += ms;
+    }
+    c->stats.abc_launches += 1;
+    c->stats.abc_trials += n;
+    return 0;
+}
+
+int abc_read_counters(epipf_ctx* c) {
+    if (c->profiling < EPIPF_PROFILE_COUNTERS) return 0;
+    HIP_TRY(hipMemcpyAsync(c->h_counters, c->counters, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride,
+                           hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    unsigned long long tot[kNumCounters] = {0, 0, 0, 0};
+    for (int sl = 0; sl < kCounterSlots; ++sl)
+        for (int k = 0; k < kNumCounters; ++k) tot[k] += c->h_counters[(size_t)sl * kCounterStride + k];
+    c->stats.events = (int64_t)tot[0];
+    c->stats.lane_iterations = (int64_t)tot[2];
+    c->stats.wave_lane_slots = (int64_t)tot[3];
+    return 0;
+}
+}  // namespace
+
+int epipf_abc_trials(epipf_ctx* c, const double* Y, int T, const double* priors, uint64_t key, uint32_t run_index,
+                     uint32_t t0, int n, double* theta_out, int32_t* rows_out, double* dist_out, int64_t* events_out) {
+    AbcPlan p;
+    if (int rc = abc_prepare(c, Y, T, priors, key, run_index, p.args)) return rc;
+    if (!theta_out) return fail(EPIPF_EINVAL, "theta_out is NULL");
+    if (n < 0 || (uint64_t)t0 + (uint64_t)n > (1ull << 32)) return fail(EPIPF_EINVAL, "trials [t0, t0+n) must lie in [0, 2^32)");
+    if (n == 0) { if (events_out) *events_out = 0; return EPIPF_OK; }
+    HIP_TRY(hipSetDevice(c->device));
+    if (int rc = abc_buffers(c, T, n, 1, p)) return rc;
+    AbcArgs a = p.args;
+    HIP_TRY(hipMemcpyAsync(p.Ydev, Y, sizeof(double) * 3 * (size_t)T, hipMemcpyHostToDevice, c->stream));
+    unsigned long long ev_before = 0;
+    const bool counting = a.count != 0;
+    if (counting) {
+        if (int rc = abc_read_counters(c)) return rc;
+        ev_before = (unsigned long long)c->stats.events;
+    }
+    if (int rc = abc_launch_trials(c, a, t0, n)) return rc;
+    std::vector<double> th((size_t)2 * n);
+    HIP_TRY(hipMemcpyAsync(th.data(), a.theta, sizeof(double) * 2 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    if (dist_out) HIP_TRY(hipMemcpyAsync(dist_out, a.dist, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    std::vector<int32_t> days;
+    if (rows_out) {
+        days.resize((size_t)3 * T * n);
+        HIP_TRY(hipMemcpyAsync(days.data(), a.days, sizeof(int32_t) * days.size(), hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (int rc = abc_account(c, n)) return rc;
+    for (int i = 0; i < n; ++i) {
+        theta_out[2 * (size_t)i] = th[i];
+        theta_out[2 * (size_t)i + 1] = th[(size_t)n + i];
+    }
+    if (rows_out)   // device [T][3][n] -> caller [n][T][3]
+        for (int d = 0; d < T; ++d)
+            for (int q = 0; q < 3; ++q)
+                for (int i = 0; i < n; ++i)
+                    rows_out[((size_t)i * T + d) * 3 + q] = days[((size_t)d * 3 + q) * n + i];
+    if (events_out) {
+        *events_out = -1;
+        if (counting) {
+            if (int rc = abc_read_counters(c)) return rc;
+            *events_out = (int64_t)((unsigned long long)c->stats.events - ev_before);
+        }
+    }
+    return EPIPF_OK;
+}
+
+int epipf_abc(epipf_ctx* c, const double* Y, int T, int no_of_samples, double threshold, const double* priors,
+              uint64_t key, uint32_t run_index, int64_t max_trials, int batch, double* theta_out, double* traj_out,
+              int64_t* trials_out, int32_t* accepted_out) {
+    AbcPlan p;
+    if (int rc = abc_prepare(c, Y, T, priors, key, run_index, p.args)) return rc;
+    if (!theta_out || !traj_out || !trials_out || !accepted_out) return fail(EPIPF_EINVAL, "NULL output pointer");
+    if (no_of_samples < 0) return fail(EPIPF_EINVAL, "no_of_samples < 0");
+    if (std::isnan(threshold)) return fail(EPIPF_EINVAL, "threshold is NaN");
+    if (max_trials < 0 || max_trials > (int64_t)(1ull << 32)) return fail(EPIPF_EINVAL, "max_trials must lie in [0, 2^32]");
+    if (batch < 0) return fail(EPIPF_EINVAL, "batch < 0");
+    *trials_out = 0;
+    *accepted_out = 0;
+    if (no_of_samples == 0) return EPIPF_OK;
+    // batch sizes: fixed, or 16k trials growing x4 per batch up to 1M (bounded so the day table stays < 4 GiB)
+    const int64_t cap_days = ((int64_t)1 << 32) / (12 * (int64_t)T);
+    const int max_batch = (int)std::max<int64_t>(256, std::min<int64_t>(batch > 0 ? batch : (1 << 20), cap_days));
+    int cur = batch > 0 ? std::min(batch, max_batch) : std::min(1 << 14, max_batch);
+    HIP_TRY(hipSetDevice(c->device));
+    if (int rc = abc_buffers(c, T, max_batch, no_of_samples, p)) return rc;
+    AbcArgs a = p.args;
+    HIP_TRY(hipMemcpyAsync(p.Ydev, Y, sizeof(double) * 3 * (size_t)T, hipMemcpyHostToDevice, c->stream));
+    int have = 0;
+    int64_t t = 0, last = -1;
+    int32_t* h_cnt = c->h_status;   // pinned staging (>= 1 entry)
+    while (have < no_of_samples && t < max_trials) {
+        const int nb = (int)std::min<int64_t>(cur, max_trials - t);
+        if (int rc = abc_launch_trials(c, a, (uint32_t)t, nb)) return rc;
+        AbcSelectArgs s{};
+        s.dist = a.dist; s.n = nb; s.need = no_of_samples - have; s.threshold = threshold; s.idx = p.idx; s.count = p.count;
+        hipError_t le = launch_abc_select(s, c->stream);
+        if (le != hipSuccess) return fail(EPIPF_EHIP, "ABC select launch failed: %s", hipGetErrorString(le));
+        AbcGatherArgs g{};
+        g.days = a.days; g.theta = a.theta; g.idx = p.idx; g.count = p.count; g.n = nb; g.T = T; g.slot0 = have;
+        g.traj = p.traj; g.theta_out = p.theta_out;
+        le = launch_abc_gather(g, no_of_samples - have, c->stream);
+        if (le != hipSuccess) return fail(EPIPF_EHIP, "ABC gather launch failed: %s", hipGetErrorString(le));
+        HIP_TRY(hipMemcpyAsync(h_cnt, p.count, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (int rc = abc_account(c, nb)) return rc;
+        const int got = h_cnt[0];
+        if (got > 0) {
+            HIP_TRY(hipMemcpyAsync(h_cnt, p.idx + got - 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            last = t + h_cnt[0];
+        }
+        have += got;
+        t += nb;
+        if (batch <= 0) cur = (int)std::min<int64_t>((int64_t)cur * 4, max_batch);
+    }
+    if (have > 0) {
+        HIP_TRY(hipMemcpyAsync(theta_out, p.theta_out, sizeof(double) * 2 * (size_t)have, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(traj_out, p.traj, sizeof(double) * 4 * (size_t)T * have, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    if (int rc = abc_read_counters(c)) return rc;
+    *accepted_out = have;
+    *trials_out = have == no_of_samples ? last + 1 : t;
+    return EPIPF_OK;
 }
 
 int epipf_set_profiling(epipf_ctx* c, int enable) {

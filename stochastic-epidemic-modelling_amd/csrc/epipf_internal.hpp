@@ -79,6 +79,40 @@ struct ResampleArgs {
     unsigned long long* fallbacks;
 };
 
+// ABC rejection (abc_algo.py:17-109).  One lane per trial; HBM layout per batch of n trials:
+//   days  int32 [T][3][n]   S, I, R at each day 0..T-1 (the reference's daily table, day column implicit)
+//   theta f64   [2][n]      beta, gamma;   dist f64 [n]
+struct AbcArgs {
+    const LogTab* logtab;
+    const double* Y;             // [T][3] observed (S, I, R)
+    int T, n, count;             // days, trials this launch, profiling counters on
+    uint32_t t0, f, k0, k1;      // first trial index, run index, Philox key
+    double prior_lo[2], prior_rng[2];   // lo and hi - lo (numpy uniform's range)
+    double lam[3], pm[3];        // initial-count means Y[0].astype(int) and their mode probabilities
+    int32_t* days;
+    double* theta;
+    double* dist;
+    unsigned long long* counters;  // [0] events, [2] lane-iterations, [3] wave-iterations x 64
+};
+
+struct AbcSelectArgs {
+    const double* dist;
+    int n, need;
+    double threshold;
+    int32_t* idx;                // [need] accepted trial offsets, in trial order
+    int32_t* count;              // [1] accepted (<= need)
+};
+
+struct AbcGatherArgs {
+    const int32_t* days;
+    const double* theta;
+    const int32_t* idx;
+    const int32_t* count;
+    int n, T, slot0;
+    double* traj;                // [samples][T][4]: day, S, I, R (abc_algo.py:56-62 column order)
+    double* theta_out;           // [samples][2]
+};
+
 size_t step_lds_bytes(int B, int wg);
 hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, hipStream_t s,
                          hipEvent_t ev_init, hipEvent_t ev_step0, hipEvent_t ev_end);
@@ -86,5 +120,8 @@ hipError_t launch_path_sample(const PathArgs& a, hipStream_t s);
 hipError_t launch_log_table(LogTab* tab, hipStream_t s);
 hipError_t launch_simulate(const SimArgs& a, int model, int G, hipStream_t s);
 hipError_t launch_resample(const ResampleArgs& a, hipStream_t s);
+hipError_t launch_abc_trials(const AbcArgs& a, hipStream_t s);
+hipError_t launch_abc_select(const AbcSelectArgs& a, hipStream_t s);
+hipError_t launch_abc_gather(const AbcGatherArgs& a, int max_count, hipStream_t s);
 
 }  // namespace epipf

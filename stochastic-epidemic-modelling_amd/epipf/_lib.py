@@ -16,12 +16,13 @@ SIR, SEIR, SIR_SUBGROUPS, SIR_SUBGROUPS2 = 0, 1, 2, 3
 OBS_BINOMIAL, OBS_NORMAL = 0, 1
 RESAMPLE_MULTINOMIAL, RESAMPLE_SYSTEMATIC = 0, 1
 PROFILE_OFF, PROFILE_TIMING, PROFILE_COUNTERS = 0, 1, 2
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 EXPORTS = (
     "epipf_create", "epipf_destroy", "epipf_set_observations", "epipf_set_population", "epipf_run",
     "epipf_copy_history", "epipf_path_sample", "epipf_simulate", "epipf_resample", "epipf_set_profiling",
     "epipf_get_stats", "epipf_reset_stats", "epipf_last_error", "epipf_abi_version", "epipf_device_count",
+    "epipf_abc", "epipf_abc_trials",
 )
 
 
@@ -37,6 +38,9 @@ class Stats(ctypes.Structure):
         ("resample_fallbacks", ctypes.c_int64),
         ("lane_iterations", ctypes.c_int64),
         ("wave_lane_slots", ctypes.c_int64),
+        ("abc_ms", ctypes.c_double),
+        ("abc_launches", ctypes.c_int64),
+        ("abc_trials", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -77,6 +81,8 @@ def load():
         "epipf_last_error": ([], ctypes.c_char_p),
         "epipf_abi_version": ([], i32),
         "epipf_device_count": ([], i32),
+        "epipf_abc": ([P, P, i32, i32, f64, P, u64, u32, ctypes.c_int64, i32, P, P, P, P], i32),
+        "epipf_abc_trials": ([P, P, i32, P, u64, u32, u32, i32, P, P, P, P], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

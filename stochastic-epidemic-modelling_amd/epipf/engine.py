@@ -152,6 +152,42 @@ class Engine:
         rc = check(self._L.epipf_resample(self._h, w.size, ptr(w), ptr(u), ptr(out), ptr(fb)), "epipf_resample")
         return (None if rc == _lib.STATUS_DEGENERATE else out), int(fb[0])
 
+    # ------------------------------------------------------------------ ABC rejection (abc_algo.py:17-109)
+    @staticmethod
+    def _abc_inputs(observed_data, priors):
+        Y = np.ascontiguousarray(np.asarray(observed_data, dtype=np.float64))
+        if Y.ndim != 2 or Y.shape[1] != 3:
+            raise ValueError("observed_data must be [T, 3] (S, I, R), as abc_algo.py:38-45 unpacks it")
+        pr = np.ascontiguousarray(np.array([priors["beta"][0], priors["beta"][1], priors["gamma"][0],
+                                            priors["gamma"][1]], dtype=np.float64))
+        return Y, pr
+
+    def abc_trials(self, observed_data, priors, key=0, run_index=0, t0=0, n=1, rows=True):
+        """Trials [t0, t0+n): theta [n,2], rows [n,T,3] int32 (S, I, R per day) or None, distance [n]."""
+        Y, pr = self._abc_inputs(observed_data, priors)
+        theta = np.empty((n, 2))
+        rw = np.empty((n, Y.shape[0], 3), dtype=np.int32) if rows else None
+        dist = np.empty(n)
+        ev = np.zeros(1, dtype=np.int64)
+        check(self._L.epipf_abc_trials(self._h, ptr(Y), Y.shape[0], ptr(pr), int(key) & (2**64 - 1),
+                                       int(run_index) & 0xFFFFFFFF, int(t0), int(n), ptr(theta), ptr(rw), ptr(dist),
+                                       ptr(ev)), "epipf_abc_trials")
+        return theta, rw, dist
+
+    def abc(self, observed_data, no_of_samples, threshold, priors, key=0, run_index=0, max_trials=2**32, batch=0):
+        """(theta [n,2], trajectories [n,T,4], trials, accepted) of epipf_abc."""
+        Y, pr = self._abc_inputs(observed_data, priors)
+        n = int(no_of_samples)
+        theta = np.empty((max(n, 1), 2))
+        traj = np.empty((max(n, 1), Y.shape[0], 4))
+        trials = np.zeros(1, dtype=np.int64)
+        acc = np.zeros(1, dtype=np.int32)
+        check(self._L.epipf_abc(self._h, ptr(Y), Y.shape[0], n, float(threshold), ptr(pr), int(key) & (2**64 - 1),
+                                int(run_index) & 0xFFFFFFFF, int(max_trials), int(batch), ptr(theta), ptr(traj),
+                                ptr(trials), ptr(acc)), "epipf_abc")
+        a = int(acc[0])
+        return theta[:a], traj[:a], int(trials[0]), a
+
     # ------------------------------------------------------------------ stats
     def set_profiling(self, level=_lib.PROFILE_COUNTERS):
         """level: PROFILE_OFF / PROFILE_TIMING (HIP events only, kernels unchanged) / PROFILE_COUNTERS

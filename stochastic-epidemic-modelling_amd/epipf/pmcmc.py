@@ -36,6 +36,7 @@ class ModelType(Enum):
 class _Stream:
     key = 0
     next_filter = 0
+    next_abc_run = 0   # ABC runs (epipf.abc) count separately: their Philox domains are disjoint
 
 
 _STREAM = _Stream()
@@ -46,6 +47,7 @@ def seed_stream(key, filter_index=0):
     the filter's own draws)."""
     _STREAM.key = int(key) & (2**64 - 1)
     _STREAM.next_filter = int(filter_index)
+    _STREAM.next_abc_run = 0
 
 
 def _take_filter_index():
