@@ -91,6 +91,7 @@ struct epipf_ctx {
     // ABC buffers (grown on demand): days, theta, dist for one batch; Y; accepted idx/count; output slots
     size_t abc_bytes = 0;
     void* abc = nullptr;
+    bool abc_order = true;   // length-ordered ABC lanes (EPIPF_ABC_ORDER=0 disables)
 };
 
 // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp): D bounds the depth of the parallel
@@ -496,12 +497,15 @@ int abc_prepare(epipf_ctx* c, const double* Y, int T, const double* priors, uint
         a.pm[q] = lam > 0.0 ? std::exp(-lam + lam * std::log(lam) - std::lgamma(lam + 1.0)) : 0.0;   // host glibc
     }
     a.T = T;
+    a.last_day = (double)(T - 1);
     a.f = run_index;
     a.k0 = (uint32_t)key;
     a.k1 = (uint32_t)(key >> 32);
     a.logtab = c->logtab;
     a.counters = c->counters;
     a.count = c->profiling >= EPIPF_PROFILE_COUNTERS ? 1 : 0;
+    c->abc_order = true;
+    if (const char* e = getenv("EPIPF_ABC_ORDER")) c->abc_order = atoi(e) != 0;
     return 0;
 }
 
@@ -512,7 +516,8 @@ int abc_buffers(epipf_ctx* c, int T, int batch, int samples, AbcPlan& p) {
                  sz_dist = align256(sizeof(double) * b), sz_Y = align256(sizeof(double) * 3 * (size_t)T),
                  sz_idx = align256(sizeof(int32_t) * (size_t)(samples + 1)), sz_cnt = 256,
                  sz_traj = align256(sizeof(double) * 4 * (size_t)T * samples), sz_to = align256(sizeof(double) * 2 * (size_t)samples);
-    const size_t need = sz_days + sz_theta + sz_dist + sz_Y + sz_idx + sz_cnt + sz_traj + sz_to;
+    const size_t sz_key = align256(sizeof(uint32_t) * b), sz_tmp = align256(abc_sort_temp_bytes(batch));
+    const size_t need = sz_days + sz_theta + sz_dist + sz_Y + sz_idx + sz_cnt + sz_traj + sz_to + 4 * sz_key + sz_tmp;
     if (need > c->abc_bytes) {
         if (c->abc) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->abc); c->abc = nullptr; c->abc_bytes = 0; }
         if (hipMalloc(&c->abc, need) != hipSuccess) return fail(EPIPF_ENOMEM, "ABC buffers hipMalloc(%zu) failed", need);
@@ -526,7 +531,14 @@ int abc_buffers(epipf_ctx* c, int T, int batch, int samples, AbcPlan& p) {
     p.idx = (int32_t*)q; q += sz_idx;
     p.count = (int32_t*)q; q += sz_cnt;
     p.traj = (double*)q; q += sz_traj;
-    p.theta_out = (double*)q;
+    p.theta_out = (double*)q; q += sz_to;
+    for (int k = 0; k < 2; ++k) {
+        p.args.sort_keys[k] = (uint32_t*)q; q += sz_key;
+        p.args.sort_vals[k] = (int32_t*)q; q += sz_key;
+    }
+    p.args.sort_temp = q;
+    p.args.sort_temp_bytes = sz_tmp;
+    p.args.perm = c->abc_order ? p.args.sort_vals[1] : nullptr;
     p.args.Y = p.Ydev;
     return 0;
 }
@@ -628,10 +640,11 @@ int epipf_abc(epipf_ctx* c, const double* Y, int T, int no_of_samples, double th
     *trials_out = 0;
     *accepted_out = 0;
     if (no_of_samples == 0) return EPIPF_OK;
-    // batch sizes: fixed, or 16k trials growing x4 per batch up to 1M (bounded so the day table stays < 4 GiB)
+    // batch sizes: fixed, or 64k trials first, then 1.25x the trials the observed acceptance rate predicts for
+    // the samples still missing (x4 while nothing is accepted), within [16k, 1M] and a day table < 4 GiB
     const int64_t cap_days = ((int64_t)1 << 32) / (12 * (int64_t)T);
     const int max_batch = (int)std::max<int64_t>(256, std::min<int64_t>(batch > 0 ? batch : (1 << 20), cap_days));
-    int cur = batch > 0 ? std::min(batch, max_batch) : std::min(1 << 14, max_batch);
+    int cur = batch > 0 ? std::min(batch, max_batch) : std::min(1 << 16, max_batch);
     HIP_TRY(hipSetDevice(c->device));
     if (int rc = abc_buffers(c, T, max_batch, no_of_samples, p)) return rc;
     AbcArgs a = p.args;
@@ -662,7 +675,11 @@ int epipf_abc(epipf_ctx* c, const double* Y, int T, int no_of_samples, double th
         }
         have += got;
         t += nb;
-        if (batch <= 0) cur = (int)std::min<int64_t>((int64_t)cur * 4, max_batch);
+        if (batch <= 0) {
+            const double want = have > 0 ? 1.25 * (double)(no_of_samples - have) * (double)t / (double)have
+                                              : 4.0 * cur;
+            cur = (int)std::max<double>(std::min<double>(want + 1024.0, (double)max_batch), std::min(1 << 14, max_batch));
+        }
     }
     if (have > 0) {
         HIP_TRY(hipMemcpyAsync(theta_out, p.theta_out, sizeof(double) * 2 * (size_t)have, hipMemcpyDeviceToHost, c->stream));

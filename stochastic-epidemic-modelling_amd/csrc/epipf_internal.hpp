@@ -86,7 +86,15 @@ struct AbcArgs {
     const LogTab* logtab;
     const double* Y;             // [T][3] observed (S, I, R)
     int T, n, count;             // days, trials this launch, profiling counters on
+    // length-ordered lanes (one lane per trial): predicted-length keys sorted with their trial offsets, lane g
+    // runs trial perm[g].  NULL: lane g runs trial g.
+    const int32_t* perm;
+    uint32_t* sort_keys[2];
+    int32_t* sort_vals[2];
+    void* sort_temp;
+    size_t sort_temp_bytes;
     uint32_t t0, f, k0, k1;      // first trial index, run index, Philox key
+    double last_day;             // T - 1 as a kernel argument (an SGPR pair; a VALU int->f64 convert would not be)
     double prior_lo[2], prior_rng[2];   // lo and hi - lo (numpy uniform's range)
     double lam[3], pm[3];        // initial-count means Y[0].astype(int) and their mode probabilities
     int32_t* days;
@@ -121,6 +129,7 @@ hipError_t launch_log_table(LogTab* tab, hipStream_t s);
 hipError_t launch_simulate(const SimArgs& a, int model, int G, hipStream_t s);
 hipError_t launch_resample(const ResampleArgs& a, hipStream_t s);
 hipError_t launch_abc_trials(const AbcArgs& a, hipStream_t s);
+size_t abc_sort_temp_bytes(int n);
 hipError_t launch_abc_select(const AbcSelectArgs& a, hipStream_t s);
 hipError_t launch_abc_gather(const AbcGatherArgs& a, int max_count, hipStream_t s);
 
