@@ -7,6 +7,12 @@
 Returned arrays drop the reference's pandas DataFrame wrapper: discrete series are [days, 1 + C] with the
 time column first (the DataFrame's column order for SIR/SEIR).  `benchmark_dataset(cfg)` builds the
 BASELINE.json configurations.
+
+Integrator ("regenerate fixtures without scipy"): the reference calls scipy's `odeint`
+(ODEPACK LSODA).  `integrator="odeint"` uses it (bit-identical to the reference); `integrator="dopri5"` is a
+numpy-only Dormand-Prince 5(4) with tight tolerances (agrees with odeint to ~1e-7 relative; the thinned
+integer datasets match it exactly unless an ODE value sits within that distance of an integer).  The default
+picks odeint when scipy imports and dopri5 otherwise.
 """
 import numpy as np
 
@@ -40,31 +46,85 @@ def differential_sir_subgroups(n_sir, t, beta, gamma):
     return tuple(out)
 
 
+# Dormand-Prince 5(4) tableau (Dormand & Prince 1980, J. Comp. Appl. Math. 6:19-26)
+_DP_C = (0.0, 1 / 5, 3 / 10, 4 / 5, 8 / 9, 1.0, 1.0)
+_DP_A = ((), (1 / 5,), (3 / 40, 9 / 40), (44 / 45, -56 / 15, 32 / 9),
+         (19372 / 6561, -25360 / 2187, 64448 / 6561, -212 / 729),
+         (9017 / 3168, -355 / 33, 46732 / 5247, 49 / 176, -5103 / 18656),
+         (35 / 384, 0.0, 500 / 1113, 125 / 192, -2187 / 6784, 11 / 84))
+_DP_E = (71 / 57600, 0.0, -71 / 16695, 71 / 1920, -17253 / 339200, 22 / 525, -1 / 40)   # 5th - 4th order
+
+
+def dopri5(f, y0, t, args=(), rtol=1e-11, atol=1e-9):
+    """odeint-compatible numpy integrator: solution [len(t), len(y0)] at the requested times (t[0] = y0)."""
+    t = np.asarray(t, dtype=np.float64)
+    y = np.asarray(y0, dtype=np.float64).copy()
+    out = np.empty((t.size, y.size))
+    out[0] = y
+
+    def rhs(tt, yy):
+        return np.asarray(f(yy, tt, *args), dtype=np.float64)
+
+    k1 = rhs(t[0], y)
+    h = 1e-3 * max(float(t[-1] - t[0]), 1e-12) if t.size > 1 else 0.0
+    for i in range(1, t.size):
+        tc, tend = t[i - 1], t[i]
+        while tc < tend:
+            h = min(h, tend - tc)
+            k = [k1]
+            for s in range(1, 7):
+                ys = y + h * sum(a * kk for a, kk in zip(_DP_A[s], k))
+                k.append(rhs(tc + _DP_C[s] * h, ys))
+            ynew = y + h * sum(a * kk for a, kk in zip(_DP_A[6], k[:6]))
+            err = h * sum(e * kk for e, kk in zip(_DP_E, k))
+            sc = atol + rtol * np.maximum(np.abs(y), np.abs(ynew))
+            en = float(np.sqrt(np.mean((err / sc) ** 2)))
+            if en <= 1.0:
+                tc = tend if tend - (tc + h) <= 1e-14 * max(1.0, abs(tend)) else tc + h
+                y = ynew
+                k1 = k[6]                                      # FSAL
+            h *= min(5.0, max(0.2, 0.9 * (1.0 / max(en, 1e-16)) ** 0.2))
+        out[i] = y
+    return out
+
+
+def _integrate(f, y0, t, args, integrator):
+    if integrator is None:
+        try:
+            import scipy.integrate  # noqa: F401
+            integrator = "odeint"
+        except ImportError:
+            integrator = "dopri5"
+    if integrator == "odeint":
+        from scipy.integrate import odeint
+        return odeint(f, y0, t, args=args)
+    if integrator == "dopri5":
+        return dopri5(f, y0, t, args)
+    raise ValueError(f"unknown integrator {integrator!r}")
+
+
 def _last_sample_per_day(t, solution):
     days = np.ceil(t).astype(int)
     rows = [int(np.nonzero(days == i)[0][-1]) for i in range(days[-1] + 1)]
     return rows
 
 
-def sir_simulate_discrete(y0, t, beta, gamma):
-    from scipy.integrate import odeint
-    sol = odeint(differential_sir, y0, t, args=(beta, gamma))
+def sir_simulate_discrete(y0, t, beta, gamma, integrator=None):
+    sol = _integrate(differential_sir, y0, t, (beta, gamma), integrator)
     rows = _last_sample_per_day(t, sol)
     return np.column_stack([np.asarray(t)[rows], sol[rows]])
 
 
-def seir_simulate_discrete(y0, t, beta, alpha, gamma):
-    from scipy.integrate import odeint
-    sol = odeint(differential_seir, y0, t, args=(beta, alpha, gamma))
+def seir_simulate_discrete(y0, t, beta, alpha, gamma, integrator=None):
+    sol = _integrate(differential_seir, y0, t, (beta, alpha, gamma), integrator)
     rows = _last_sample_per_day(t, sol)
     return np.column_stack([np.asarray(t)[rows], sol[rows]])
 
 
-def sir_subgroups_simulate_discrete(y0, t, beta, gamma):
+def sir_subgroups_simulate_discrete(y0, t, beta, gamma, integrator=None):
     """Columns: S0, I0, R0, S1, ... then time LAST (pmcmc.py:99-113 DataFrame order)."""
-    from scipy.integrate import odeint
     y0 = [i for item in np.asarray(y0).tolist() for i in item]
-    sol = odeint(differential_sir_subgroups, y0, t, args=(np.asarray(beta).tolist(), gamma))
+    sol = _integrate(differential_sir_subgroups, y0, t, (np.asarray(beta).tolist(), gamma), integrator)
     rows = _last_sample_per_day(t, sol)
     return np.column_stack([sol[rows], np.asarray(t)[rows]])
 
@@ -77,34 +137,39 @@ def noise_normal(values, ratio, rs):
     return np.array([[rs.normal(v, ratio * v) for v in row] for row in values]).astype(int).astype(np.float64)
 
 
-def benchmark_dataset(cfg):
+def benchmark_dataset(cfg, integrator=None):
     """Observation matrices for the BASELINE.json configs.  Returns (Y, meta)."""
     if cfg == 1:
-        ode = sir_simulate_discrete((180, 20, 0), np.linspace(0, 49, num=500), 2, 1)[:, 1:]
+        ode = sir_simulate_discrete((180, 20, 0), np.linspace(0, 49, num=500), 2, 1,
+                                    integrator=integrator)[:, 1:]
         return thin_binomial(ode, 0.1, np.random.RandomState(2)), dict(
             model="sir", n_population=200, mu=20, theta=(2.0, 1.0), probs=0.1, N=100,
             describe="ODE SIR y0=(180,20,0), beta=2, gamma=1, 50 daily rows, binomial thinning p=.1, RandomState(2)")
     if cfg == 2:
-        ode = sir_simulate_discrete((9980, 20, 0), np.linspace(0, 199, num=2000), 0.25, 0.1)[:, 1:]
+        ode = sir_simulate_discrete((9980, 20, 0), np.linspace(0, 199, num=2000), 0.25, 0.1,
+                                    integrator=integrator)[:, 1:]
         return thin_binomial(ode, 0.1, np.random.RandomState(1)), dict(
             model="sir", n_population=10000, mu=20, theta=(0.25, 0.1), probs=0.1, N=10000,
             describe="ODE SIR y0=(9980,20,0), beta=.25, gamma=.1, 200 daily rows, binomial thinning p=.1, "
                      "RandomState(1)")
     if cfg == 3:
-        ode = seir_simulate_discrete((9980, 0, 20, 0), np.linspace(0, 199, num=2000), 0.5, 0.2, 0.1)[:, 1:]
+        ode = seir_simulate_discrete((9980, 0, 20, 0), np.linspace(0, 199, num=2000), 0.5, 0.2, 0.1,
+                                     integrator=integrator)[:, 1:]
         return noise_normal(ode, 0.1, np.random.RandomState(3)), dict(
             model="seir", n_population=10000, mu=20, theta=(0.5, 0.2, 0.1), probs=0.1, observations=True, N=10000,
             describe="ODE SEIR y0=(9980,0,20,0), beta=.5, alpha=.2, gamma=.1, 200 daily rows, Gaussian noise "
                      "N(x, .1x) cast to int, RandomState(3); normal observation model")
     if cfg == 4:
-        ode = sir_simulate_discrete((4800, 20, 0), np.linspace(0, 14, num=200), 2, 1)[:, 1:]
+        ode = sir_simulate_discrete((4800, 20, 0), np.linspace(0, 14, num=200), 2, 1,
+                                    integrator=integrator)[:, 1:]
         return thin_binomial(ode, 0.1, np.random.RandomState(11)), dict(
             model="sir", n_population=4820, mu=20, theta=(2.0, 1.0), probs=0.1, N=50000,
             describe="ODE SIR y0=(4800,20,0), beta=2, gamma=1, 15 daily rows, binomial thinning p=.1 "
                      "(under-reported counts), RandomState(11)")
     if cfg == 5:
         pop = np.array([[2000, 30, 0], [3000, 40, 0]])
-        ode = sir_subgroups_simulate_discrete(pop, np.linspace(0, 14, num=200), np.array([[5, 2], [1, 3]]), 0.5)
+        ode = sir_subgroups_simulate_discrete(pop, np.linspace(0, 14, num=200), np.array([[5, 2], [1, 3]]), 0.5,
+                                              integrator=integrator)
         return thin_binomial(ode[:, :6], 0.1, np.random.RandomState(14)), dict(
             model="sir_subgroups", n_population=[2030, 3040], mu=[30, 40], theta=[4.0, 1.0, 1.0, 4.0, 1.0],
             probs=0.1, N=10000,
