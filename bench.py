@@ -214,6 +214,9 @@ def main():
             "ssa_lane_utilisation": lane_use,
             "resample_fallbacks": st["resample_fallbacks"],
             "events_per_particle_step": cst["events"] / cst["particle_steps"] if cst["particle_steps"] else None,
+            # particle-steps the certified f32 SSA path handed to the exact loop, and waves that waited on one
+            "ssa_exact_particle_frac": cst["ssa_exact_lanes"] / cst["particle_steps"] if cst["particle_steps"] else None,
+            "ssa_exact_wave_frac": cst["ssa_exact_waves"] * 64 / cst["particle_steps"] if cst["particle_steps"] else None,
             "gathered_draws_shape": list(gathered.shape),
             "cpu_baseline": base,
         }

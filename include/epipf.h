@@ -82,6 +82,8 @@ typedef struct {
     double abc_ms;               /* HIP-event time of the ABC trial kernels (profiling on) */
     int64_t abc_launches;        /* ABC trial kernel launches */
     int64_t abc_trials;          /* ABC trials simulated (accepted or not) */
+    int64_t ssa_exact_lanes;     /* filter particle-steps simulated on the exact f64 SSA loop (profiling counters) */
+    int64_t ssa_exact_waves;     /* filter wave-steps with at least one such particle-step */
 } epipf_stats;
 
 /* groups: G for the subgroup models (1 <= G <= 4), ignored (1) for SIR/SEIR.

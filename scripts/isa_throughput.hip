@@ -52,6 +52,14 @@ OP_KERNEL(k_cvt_f64_u32, double, 1.0, "v_cvt_f64_u32 %0, %1", : "v"(7u))
 OP_KERNEL(k_cmp_f64, uint32_t, 1, "v_cmp_lt_f64 vcc, %1, %2\n\tv_cndmask_b32 %0, %0, 0, vcc", : "v"(1.0), "v"(2.0) : "vcc")
 OP_KERNEL(k_cndmask, uint32_t, 1, "v_cmp_lt_u32 vcc, %0, %1\n\tv_cndmask_b32 %0, %0, 0, vcc", : "v"(7u) : "vcc")
 OP_KERNEL(k_pk_fma_f32, double, 1.0, "v_pk_fma_f32 %0, %0, %1, %1", : "v"(0.999))
+OP_KERNEL(k_bitop3, uint32_t, 1, "v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96", : "v"(0x1234u))
+OP_KERNEL(k_bitop3_s, uint32_t, 1, "v_bitop3_b32 %0, %0, %1, %0 bitop3:0x96", : "s"(0x1234u))
+OP_KERNEL(k_mul_f32, float, 1.0f, "v_mul_f32 %0, %0, %1", : "v"(0.999f))
+OP_KERNEL(k_add_f32, float, 1.0f, "v_add_f32 %0, %0, %1", : "v"(0.999f))
+OP_KERNEL(k_cvt_f32_u32, float, 1.0f, "v_cvt_f32_u32 %0, %1", : "v"(7u))
+OP_KERNEL(k_pk_mul_f32, double, 1.0, "v_pk_mul_f32 %0, %0, %1", : "v"(0.999))
+OP_KERNEL(k_pk_add_f32, double, 1.0, "v_pk_add_f32 %0, %0, %1", : "v"(0.999))
+OP_KERNEL(k_exp_f32, float, 1.0f, "v_exp_f32 %0, %0", )
 // random-operand probes: the value stays a full-width random word (each is 2 instructions: op + xor-fold)
 #define RND(NAME, OPASM) OP_KERNEL(NAME, uint32_t, 0x9E3779B9u * 7, OPASM "\n\tv_xor_b32 %0, %0, v44", : "v"(0xD2511F53u) : "v44")
 RND(k_r_mulhi, "v_mul_hi_u32 v44, %0, %1")
@@ -144,6 +152,23 @@ int main(int argc, char** argv) {
             run<uint32_t, 8>("r mad64+xor", k_r_mad<8>, b, 0.0);
             run<double, 8>("r fma64+fract", k_r_fma64<8>, b, 0.0);
         }
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'b') {   // gfx950 three-input bitop and f32 candidates for the event loop
+        BOTH(k_xor, uint32_t)
+        BOTH(k_bitop3, uint32_t)
+        BOTH(k_bitop3_s, uint32_t)
+        BOTH(k_mul_f32, float)
+        BOTH(k_add_f32, float)
+        BOTH(k_fma_f32, float)
+        BOTH(k_cvt_f32_u32, float)
+        BOTH(k_pk_mul_f32, double)
+        BOTH(k_pk_add_f32, double)
+        BOTH(k_pk_fma_f32, double)
+        BOTH(k_log_f32, float)
+        BOTH(k_exp_f32, float)
+        BOTH(k_rcp_f32, float)
+        BOTH(k_mad_u64, uint64_t)
         return 0;
     }
     if (argc > 1 && argv[1][0] == 's') {   // loop-body size probe at 8 waves/SIMD (kIters scaled by the host)

@@ -92,6 +92,7 @@ struct epipf_ctx {
     size_t abc_bytes = 0;
     void* abc = nullptr;
     bool abc_order = true;   // length-ordered ABC lanes (EPIPF_ABC_ORDER=0 disables)
+    bool fast_ssa = true;    // SIR certified f32 event loop (EPIPF_SSA_FAST=0 disables; results are identical)
 };
 
 // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp): D bounds the depth of the parallel
@@ -152,6 +153,7 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     c->Tmax = t_max;
     c->max_chains = max_chains;
     c->wg = default_wg(n_particles);
+    if (const char* e = getenv("EPIPF_SSA_FAST")) c->fast_ssa = atoi(e) != 0;
     c->B = (n_particles + c->wg - 1) / c->wg;
     if (step_lds_bytes(c->B, c->wg) > 160 * 1024) {
         free_ctx(c);
@@ -275,6 +277,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
         q.k0 = (uint32_t)keys[ch];
         q.k1 = (uint32_t)(keys[ch] >> 32);
         q.f = filter_index[ch];
+        q.flags = c->fast_ssa ? kChainFastSsa : 0u;
         c->h_status[ch] = on ? EPIPF_STATUS_OK : EPIPF_STATUS_SKIPPED;
         n_active += on;
     }
@@ -326,13 +329,15 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
         c->stats.step_ms += ms_step;
         c->stats.step_launches += c->T - 1;
     }
-    unsigned long long tot[kNumCounters] = {0, 0, 0, 0};
+    unsigned long long tot[kNumCounters] = {0, 0, 0, 0, 0, 0};
     for (int sl = 0; sl < kCounterSlots; ++sl)
         for (int k = 0; k < kNumCounters; ++k) tot[k] += c->h_counters[(size_t)sl * kCounterStride + k];
     c->stats.events = (int64_t)tot[0];
     c->stats.resample_fallbacks = (int64_t)tot[1];
     c->stats.lane_iterations = (int64_t)tot[2];
     c->stats.wave_lane_slots = (int64_t)tot[3];
+    c->stats.ssa_exact_lanes = (int64_t)tot[4];
+    c->stats.ssa_exact_waves = (int64_t)tot[5];
     c->stats.particle_steps += (int64_t)n_active * c->N * c->T;
     c->stats.filters += n_active;
     c->last_chains = n_chains;
@@ -410,6 +415,7 @@ int epipf_simulate(epipf_ctx* c, int n, const int32_t* states_in, const double* 
     memset(&q, 0, sizeof q);
     for (int i = 0; i < d; ++i) q.theta[i] = theta[i];
     q.k0 = (uint32_t)key; q.k1 = (uint32_t)(key >> 32); q.f = filter_index;
+    q.flags = c->fast_ssa ? kChainFastSsa : 0u;
     HIP_TRY(hipMemcpyAsync(dcp, &q, sizeof q, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(din, states_in, sizeof(int32_t) * (size_t)n * c->C, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(dev_events, 0, sizeof(unsigned long long), c->stream));
@@ -570,7 +576,7 @@ int abc_read_counters(epipf_ctx* c) {
     HIP_TRY(hipMemcpyAsync(c->h_counters, c->counters, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride,
                            hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    unsigned long long tot[kNumCounters] = {0, 0, 0, 0};
+    unsigned long long tot[kNumCounters] = {0, 0, 0, 0, 0, 0};
     for (int sl = 0; sl < kCounterSlots; ++sl)
         for (int k = 0; k < kNumCounters; ++k) tot[k] += c->h_counters[(size_t)sl * kCounterStride + k];
     c->stats.events = (int64_t)tot[0];

@@ -26,11 +26,21 @@ struct Block { uint32_t x, y, z, w; };
 
 __device__ __forceinline__ Block philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
                                         uint32_t k1) {
+    // Rounds 0-2 keep plain XORs: with a wave-uniform counter word and key, the compiler runs most of them on
+    // the scalar unit.  From round 3 on every word is lane-varying and each three-way XOR is one gfx950
+    // v_bitop3_b32 (truth table 0x96) instead of two v_xor_b32: 14 fewer VALU instructions per block.
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         const uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;   // one 32x32->64 multiply each
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n0, n2;
+        if (r < 3) {
+            n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+            n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        } else {
+            n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+            n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
+        }
         c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }
@@ -60,8 +70,9 @@ struct ChainParam {
     double logp, log1mp;       // log(p), log1p(-p)  (host glibc, identical to the oracle's)
     uint32_t k0, k1;           // Philox key
     uint32_t f;                // filter index
-    uint32_t pad;
+    uint32_t flags;            // kChainFastSsa: the SIR certified f32 event loop may run (EPIPF_SSA_FAST=0 clears it)
 };
+constexpr uint32_t kChainFastSsa = 1u;
 
 // ------------------------------------------------------------------------------- f64 log, table driven
 // log(x) for normal x > 0, within 1 ulp of glibc's correctly rounded log (exact near x = 1).  x = 2^k z with
@@ -336,13 +347,102 @@ struct SubgroupsState {                                                // gilles
 template <int G> struct SsaState<kSubgroups, G> : SubgroupsState<G> {};
 template <int G> struct SsaState<kSubgroups2, G> : SubgroupsState<G> {};
 
+// ------------------------------------------------------------------------------- SIR f32 fast path
+// The exact loop above spends ~45 f64 operations per event (the table log alone ~20, v_rcp_f64 16 cycles).
+// The fast path takes every decision in f32 and certifies it (derivation: DESIGN.md §4):
+//   channel  q = a0 * rcp(as) is within 2^-20 of the reference's ratio (a0: 3 roundings, as: 4, v_rcp_f32
+//            <= 1.53 ulp, product 1).  U lies in [uf, uf + 2^-23) for uf its top 23 bits; with uc = uf + 2^-24,
+//            the decision q_ref <= U is certain when |q - uc| > 2^-19, else sir_channel_exact decides.
+//   clock    time is kept in units of 1/ln 2 and counted down: rem = tmax/ln2 + sum(log2(x_f) * rcp(as)), the
+//            event is inside the step iff rem >= 0 (the exact path's t + tau <= tmax, scaled).  x_f = 1 - U from
+//            two converts (relative error <= 3 * 2^-24 for x >= 2^-20); v_log_f32 is within 2 ulp of |log2 x| on
+//            every float in [2^-20, 1), v_rcp_f32 within 1.53 ulp (exhaustive, scripts/f32_accuracy.hip).  Per
+//            event |tau2_f - tau2| <= 9.6*2^-24 |tau2_f| + 4.4*2^-24 rcp(as), so with R = sum rcp(as) the
+//            remaining time is within B = 11*2^-24 tmax/ln2 + 5*2^-24 R (float rounding of B and rem included)
+//            of the exact path's, scaled.  rem > B: the event is the exact path's; rem < -B: the step ends
+//            there, as in the exact path; otherwise (and for x < 2^-20, probability 2^-20 per event) the lane
+//            hands its whole step to the exact loop, from the untouched parent state.
+// Eligible lanes: N < 2^24 (counts exact in f32; at most 2N < 2^25 events per step) and beta/N, gamma zero or
+// in [2^-60, 2^40] / [2^-60, 2^60] (every f32 intermediate stays normal).
+constexpr float kChanBandF = 0x1.0p-19f;
+constexpr float kClockTmaxF = 11.0f * 0x1.0p-24f;
+constexpr float kClockRF = 5.0f * 0x1.0p-24f;
+constexpr double kInvLn2 = 0x1.71547652b82fep0;
+
+__device__ __forceinline__ bool sir_fast_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
+                                                   double tmax, int& nev_out, int& iters) {
+    const double N = (x[0] + x[1]) + x[2];
+    const float bN = (float)(cp.theta[0] / N), g = (float)cp.theta[1];
+    iters = 0;
+    nev_out = 0;
+    if (!(cp.flags & kChainFastSsa)) return false;
+    if (!(N < 16777216.0 && (bN == 0.f || (bN >= 0x1.0p-60f && bN <= 0x1.0p40f)) &&
+          (g == 0.f || (g >= 0x1.0p-60f && g <= 0x1.0p60f))))
+        return false;
+    float S = (float)x[0], I = (float)x[1];
+    double rem = tmax * kInvLn2;                                       // remaining time, units of 1/ln 2
+    const float Bt = (float)rem * kClockTmaxF;
+    float R = 0.f, df = 0.f, B = 0.f;
+    int nrec = 0;
+    uint32_t k = 0;
+    bool alive = I > 0.f, ok = true, tiny = false;
+    Block rn{0u, 0u, 0u, 0u};
+    if (alive) rn = philox(0u, j, ptag, cp.f, cp.k0, cp.k1);
+    while (alive) {
+        const Block r = rn;
+        ++k;
+        rn = philox(__builtin_amdgcn_readfirstlane(k), j, ptag, cp.f, cp.k0, cp.k1);
+        const float a0 = bN * (S * I);                                 // gillespie_algo.py:38
+        const float as = fmaf(g, I, a0);                               // :39, :62
+        const float ri = __builtin_amdgcn_rcpf(as);
+        const float q = a0 * ri;
+        const float uc = __uint_as_float(0x3F800000u | (r.w >> 9)) - (1.0f - 0x1.0p-24f);   // uf + 2^-24
+        bool second = q < uc;                                          // choice(2, p=a/sum(a)), :63
+        if (fabsf(q - uc) <= kChanBandF)
+            second = sir_channel_exact(cp.theta[0], cp.theta[1], (double)S, (double)I, N, u01(r.z, r.w));
+        const uint32_t nh = ~r.y;
+        const float xf = fmaf((float)nh, 0x1.0p-32f, (float)(~r.x) * 0x1.0p-64f);   // 1 - U
+        const double rn_time = rem + (double)(__builtin_amdgcn_logf(xf) * ri);      // exponential, :62
+        R += ri;
+        df = (float)rn_time;
+        B = fmaf(R, kClockRF, Bt);
+        tiny = nh < 4096u;
+        ok = df > B && !tiny;                                          // certainly inside the step, :65-66
+        if (ok) {
+            rem = rn_time;
+            S = S - (second ? 0.f : 1.f);
+            I = I + (second ? -1.f : 1.f);
+            nrec += second ? 1 : 0;
+        }
+        alive = ok && I > 0.f;
+    }
+    iters = (int)k;
+    if (!ok && (tiny || !(df < -B))) return false;                     // boundary too close to call
+    x[0] = (double)S;
+    x[1] = (double)I;
+    x[2] = x[2] + (double)nrec;
+    nev_out = (int)k - (ok ? 0 : 1);                                   // every iteration but an overshoot applies
+    return true;
+}
+
 // One particle over [0, tmax] (every lane of the wave starts together, so the event index k is wave-uniform).
 // Software pipelining: event k+1's Philox block (counter-based, so independent of event k's outcome) is
 // computed while event k's f64 work runs, which gives each wave two independent dependency chains.  The
-// block drawn after the last event is discarded (one per particle-step).
+// block drawn after the last event is discarded (one per particle-step).  SIR lanes first try the certified
+// f32 path; lanes it cannot certify run this exact loop from the untouched parent state.
 template <int MODEL, int G>
 __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
-                                             double tmax, const LogTab* __restrict__ tab, int& iters) {
+                                             double tmax, const LogTab* __restrict__ tab, int& iters, int& exact) {
+    int fast_iters = 0;
+    exact = 1;
+    if constexpr (MODEL == kSIR) {
+        int nev = 0;
+        if (sir_fast_propagate(x, cp, j, ptag, tmax, nev, fast_iters)) {
+            iters = fast_iters;
+            exact = 0;
+            return nev;
+        }
+    }
     SsaState<MODEL, G> st;
     st.load(x, cp);
     double t = 0.0;
@@ -360,7 +460,7 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
         alive = ev && st.active();
     }
     st.save(x);
-    iters = (int)k;
+    iters = (int)k + fast_iters;
     return nev;
 }
 

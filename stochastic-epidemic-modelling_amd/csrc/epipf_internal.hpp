@@ -11,7 +11,7 @@ namespace epipf {
 // (~10 ns each on MI355X), which at 5k waves per launch cost more than the launch itself.
 constexpr int kCounterSlots = 64;
 constexpr int kCounterStride = 16;   // u64 per slot = 128 B
-constexpr int kNumCounters = 4;
+constexpr int kNumCounters = 6;
 
 __device__ __forceinline__ unsigned long long* counter_slot(unsigned long long* base) {
     return base + (size_t)((blockIdx.x + 7u * blockIdx.y) & (kCounterSlots - 1)) * kCounterStride;
@@ -41,7 +41,8 @@ struct StepArgs {
     double* log_zeta;
     int32_t* status;
     unsigned long long* counters;  // [kCounterSlots][kCounterStride]: [0] events, [1] resample fallbacks,
-                                   // [2] SSA lane-iterations, [3] wave-iterations x 64 (summed on the host)
+                                   // [2] SSA lane-iterations, [3] wave-iterations x 64, [4] particle-steps on
+                                   // the exact SSA loop, [5] waves with one (summed on the host)
     double npop[kMaxG], mu[kMaxG], emu[kMaxG];
     int kmax[kMaxG];
 };

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
     if (blockIdx.x == 0 && tid == 0)
         a.log_zeta[(size_t)chain * a.T + p] = a.log_zeta[(size_t)chain * a.T + p - 1] + log(total / (double)a.N);
 
-    int nev = 0, iters = 0;
+    int nev = 0, iters = 0, exact = 0;
     double w = 0.0;
     // (d) multinomial (or systematic) draw and certified search, pmcmc.py:188-190
     double U = 0.0;
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
 #pragma unroll
         for (int c = 0; c < C; ++c) x[c] = (double)hp[c];
         const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
-        nev = ssa_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, tab, iters);
+        nev = ssa_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, tab, iters, exact);
         int32_t* hc = a.hidden + (size_t)chain * a.hist_stride + ((size_t)p * a.N + j) * C;
 #pragma unroll
         for (int c = 0; c < C; ++c) hc[c] = (int32_t)x[c];                        // :222-231
@@ -167,11 +167,14 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
             li += __shfl_xor(li, o, 64);
             wmax = max(wmax, __shfl_xor(wmax, o, 64));
         }
+        const unsigned long long ex = __ballot(exact != 0);
         if ((tid & 63) == 0) {
             unsigned long long* slot = counter_slot(a.counters);
             atomicAdd(slot, e);
             atomicAdd(slot + 2, li);
             atomicAdd(slot + 3, 64ull * (unsigned long long)wmax);
+            atomicAdd(slot + 4, (unsigned long long)__popcll(ex));        // lanes on the exact SSA loop
+            atomicAdd(slot + 5, ex ? 1ull : 0ull);                        // waves with at least one
         }
     }
     if (p + 1 < a.T) {
@@ -212,7 +215,8 @@ __global__ __launch_bounds__(256) void simulate_kernel(SimArgs a) {
         double x[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) x[c] = (double)a.in[(size_t)j * C + c];
-        nev = ssa_propagate<MODEL, G>(x, *a.cp, (uint32_t)j, (a.step & 0xFFFFFFu) | kDomainSSA, a.tmax, tab, iters);
+        int exact = 0;
+        nev = ssa_propagate<MODEL, G>(x, *a.cp, (uint32_t)j, (a.step & 0xFFFFFFu) | kDomainSSA, a.tmax, tab, iters, exact);
 #pragma unroll
         for (int c = 0; c < C; ++c) a.out[(size_t)j * C + c] = (int32_t)x[c];
     }

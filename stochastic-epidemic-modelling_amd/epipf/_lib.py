@@ -41,6 +41,8 @@ class Stats(ctypes.Structure):
         ("abc_ms", ctypes.c_double),
         ("abc_launches", ctypes.c_int64),
         ("abc_trials", ctypes.c_int64),
+        ("ssa_exact_lanes", ctypes.c_int64),
+        ("ssa_exact_waves", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -297,3 +297,61 @@ def test_full_size_cfg2_properties(datasets_golden):
     np.testing.assert_array_equal(hid[0], o["hidden"])
     np.testing.assert_array_equal(anc[0], o["ancestry"])
     np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-8)
+
+
+def _engine_with_fast_ssa(enabled, N, T, chains):
+    """A fresh context with the certified f32 SIR event loop on or off (EPIPF_SSA_FAST is read at create)."""
+    import os
+    from epipf.engine import Engine
+    old = os.environ.get("EPIPF_SSA_FAST")
+    os.environ["EPIPF_SSA_FAST"] = "1" if enabled else "0"
+    try:
+        return Engine("sir", 1, N, T, chains)
+    finally:
+        if old is None:
+            del os.environ["EPIPF_SSA_FAST"]
+        else:
+            os.environ["EPIPF_SSA_FAST"] = old
+
+
+def test_fast_ssa_path_equals_exact_path_at_scale(datasets_golden):
+    """Config-2-sized filters (N = 10^4, T = 200, 8 chains, ~1.4e9 events): the certified f32 event loop and
+    the f64 loop give bit-identical states, ancestors and likelihoods.  At this size a few thousand particle-
+    steps take the replay path and a few thousand events the exact channel fallback."""
+    Y = datasets_golden["cfg2_binom"]
+    T, N, C = Y.shape[0], 10000, 8
+    th = np.array([[0.25, 0.1], [0.3, 0.1], [0.2, 0.12], [0.25, 0.08], [0.5, 0.2], [0.25, 0.1], [0.4, 0.3],
+                   [0.1, 0.05]])
+    out = []
+    for fast in (True, False):
+        eng = _engine_with_fast_ssa(fast, N, T, C)
+        eng.set_observations(Y)
+        eng.set_population(10000.0, 20.0)
+        eng.set_profiling(2)
+        lz, st = eng.run(th, [0.1] * C, [11 + c for c in range(C)], [3] * C)
+        hid, anc = eng.history(C)
+        out.append((lz, st, hid, anc, eng.stats()))
+        eng.close()
+    (lz1, st1, h1, a1, s1), (lz0, st0, h0, a0, s0) = out
+    np.testing.assert_array_equal(st1, st0)
+    np.testing.assert_array_equal(h1, h0)
+    np.testing.assert_array_equal(a1, a0)
+    np.testing.assert_array_equal(lz1, lz0)
+    assert s1["events"] == s0["events"]
+    assert 0 < s1["ssa_exact_lanes"] < 1e-2 * C * N * T      # replays happen, rarely
+
+
+def test_fast_ssa_simulate_equals_exact_path():
+    """epipf_simulate over assorted horizons and parameters, fast path on vs off (same bits)."""
+    rs = np.random.RandomState(5)
+    n = 20000
+    st = np.stack([9000 - rs.randint(0, 3000, n), rs.randint(0, 900, n), rs.randint(0, 100, n)], 1)
+    for theta, tmax in (((0.25, 0.1), 1.0), ((2.0, 1.0), 0.37), ((1.5, 0.5), 2.5), ((0.0, 0.3), 1.0),
+                        ((3.0, 0.0), 1.0), ((1e-9, 1e-9), 1.0)):
+        res = []
+        for fast in (True, False):
+            eng = _engine_with_fast_ssa(fast, 1, 1, 1)
+            res.append(eng.simulate(st, np.array(theta), tmax, key=9, filter_index=1, step=4))
+            eng.close()
+        np.testing.assert_array_equal(res[0][0], res[1][0])
+        assert res[0][1] == res[1][1]
