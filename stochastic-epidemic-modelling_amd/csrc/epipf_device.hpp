@@ -24,13 +24,16 @@ enum Obs : int { kBinomial = 0, kNormal = 1 };
 // Salmon et al. SC'11; constants and key schedule of Random123.  Counter words: (c0, c1, c2, c3).
 struct Block { uint32_t x, y, z, w; };
 
+// INVX: return ~x (the last round's three-way XOR with truth table 0x69 instead of 0x96, no extra instruction);
+// the f32 event loop needs 1 - U, whose low word is ~x.
+template <bool INVX = false>
 __device__ __forceinline__ Block philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
                                         uint32_t k1) {
     // Rounds 0-2 keep plain XORs: with a wave-uniform counter word and key, the compiler runs most of them on
     // the scalar unit.  From round 3 on every word is lane-varying and each three-way XOR is one gfx950
     // v_bitop3_b32 (truth table 0x96) instead of two v_xor_b32: 14 fewer VALU instructions per block.
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < 9; ++r) {
         const uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;   // one 32x32->64 multiply each
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
         uint32_t n0, n2;
@@ -44,7 +47,11 @@ __device__ __forceinline__ Block philox(uint32_t c0, uint32_t c1, uint32_t c2, u
         c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }
-    return Block{c0, c1, c2, c3};
+    constexpr unsigned kLastX = INVX ? 0x69u : 0x96u;               // round 9
+    const uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
+    return Block{(uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, kLastX), (uint32_t)p1,
+                 (uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96), (uint32_t)p0};
 }
 
 // 53-bit uniform in [0, 1): ((hi << 32 | lo) >> 11) * 2^-53  (numpy's Philox double convention).
@@ -379,49 +386,50 @@ __device__ __forceinline__ bool sir_fast_propagate(double* x, const ChainParam& 
     if (!(N < 16777216.0 && (bN == 0.f || (bN >= 0x1.0p-60f && bN <= 0x1.0p40f)) &&
           (g == 0.f || (g >= 0x1.0p-60f && g <= 0x1.0p60f))))
         return false;
-    float S = (float)x[0], I = (float)x[1];
+    const float S0 = (float)x[0], SI0 = (float)x[0] + (float)x[1];
+    float S = S0, I = (float)x[1];
     double rem = tmax * kInvLn2;                                       // remaining time, units of 1/ln 2
     const float Bt = (float)rem * kClockTmaxF;
     float R = 0.f, df = 0.f, B = 0.f;
-    int nrec = 0;
-    uint32_t k = 0;
-    bool alive = I > 0.f, ok = true, tiny = false;
+    uint32_t ks = 0;                                                   // event index, wave-uniform (SGPR)
+    bool alive = I > 0.f, ok = true, tiny = false, second = false;
     Block rn{0u, 0u, 0u, 0u};
-    if (alive) rn = philox(0u, j, ptag, cp.f, cp.k0, cp.k1);
+    if (alive) rn = philox<true>(0u, j, ptag, cp.f, cp.k0, cp.k1);    // x word inverted: ~x
     while (alive) {
         const Block r = rn;
-        ++k;
-        rn = philox(__builtin_amdgcn_readfirstlane(k), j, ptag, cp.f, cp.k0, cp.k1);
+        ks = __builtin_amdgcn_readfirstlane(ks) + 1u;
+        rn = philox<true>(ks, j, ptag, cp.f, cp.k0, cp.k1);
         const float a0 = bN * (S * I);                                 // gillespie_algo.py:38
         const float as = fmaf(g, I, a0);                               // :39, :62
         const float ri = __builtin_amdgcn_rcpf(as);
         const float q = a0 * ri;
         const float uc = __uint_as_float(0x3F800000u | (r.w >> 9)) - (1.0f - 0x1.0p-24f);   // uf + 2^-24
-        bool second = q < uc;                                          // choice(2, p=a/sum(a)), :63
+        second = q < uc;                                               // choice(2, p=a/sum(a)), :63
         if (fabsf(q - uc) <= kChanBandF)
             second = sir_channel_exact(cp.theta[0], cp.theta[1], (double)S, (double)I, N, u01(r.z, r.w));
         const uint32_t nh = ~r.y;
-        const float xf = fmaf((float)nh, 0x1.0p-32f, (float)(~r.x) * 0x1.0p-64f);   // 1 - U
-        const double rn_time = rem + (double)(__builtin_amdgcn_logf(xf) * ri);      // exponential, :62
+        const float xf = fmaf((float)nh, 0x1.0p-32f, (float)r.x * 0x1.0p-64f);     // 1 - U (r.x is ~x)
+        rem = rem + (double)(__builtin_amdgcn_logf(xf) * ri);          // exponential, :62
         R += ri;
-        df = (float)rn_time;
+        df = (float)rem;
         B = fmaf(R, kClockRF, Bt);
         tiny = nh < 4096u;
         ok = df > B && !tiny;                                          // certainly inside the step, :65-66
-        if (ok) {
-            rem = rn_time;
-            S = S - (second ? 0.f : 1.f);
-            I = I + (second ? -1.f : 1.f);
-            nrec += second ? 1 : 0;
-        }
+        S = S - (second ? 0.f : 1.f);                                  // applied unconditionally; a lane that
+        I = I + (second ? -1.f : 1.f);                                 // fails `ok` leaves and undoes it below
         alive = ok && I > 0.f;
     }
-    iters = (int)k;
-    if (!ok && (tiny || !(df < -B))) return false;                     // boundary too close to call
+    if (!ok) {
+        if (tiny || !(df < -B)) return false;                         // boundary too close to call: exact loop
+        S = S + (second ? 0.f : 1.f);                                  // the overshooting event is not applied
+        I = I - (second ? -1.f : 1.f);
+    }
+    const float infections = S0 - S, recoveries = SI0 - (S + I);
     x[0] = (double)S;
     x[1] = (double)I;
-    x[2] = x[2] + (double)nrec;
-    nev_out = (int)k - (ok ? 0 : 1);                                   // every iteration but an overshoot applies
+    x[2] = x[2] + (double)recoveries;
+    nev_out = (int)(infections + recoveries);
+    iters = nev_out + (ok ? 0 : 1);
     return true;
 }
 
