@@ -92,7 +92,7 @@ struct epipf_ctx {
     size_t abc_bytes = 0;
     void* abc = nullptr;
     bool abc_order = true;   // length-ordered ABC lanes (EPIPF_ABC_ORDER=0 disables)
-    bool fast_ssa = true;    // SIR certified f32 event loop (EPIPF_SSA_FAST=0 disables; results are identical)
+    bool fast_ssa = true;    // certified f32 event loop (EPIPF_SSA_FAST=0 disables; results are identical)
 };
 
 // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp): D bounds the depth of the parallel
@@ -270,6 +270,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
             if (on && !(v >= 0.0 && v < INFINITY))
                 return fail(EPIPF_EINVAL, "theta[%d][%d]=%g: parameters must be finite and >= 0 (pmcmc.py:333)", ch, i, v);
             q.theta[i] = v;
+            q.thetaf[i] = (float)v;
         }
         q.probs = probs[ch];
         q.logp = std::log(probs[ch]);
@@ -413,7 +414,7 @@ int epipf_simulate(epipf_ctx* c, int n, const int32_t* states_in, const double* 
     unsigned long long* dev_events = (unsigned long long*)((char*)dout + sb);
     ChainParam q;
     memset(&q, 0, sizeof q);
-    for (int i = 0; i < d; ++i) q.theta[i] = theta[i];
+    for (int i = 0; i < d; ++i) { q.theta[i] = theta[i]; q.thetaf[i] = (float)theta[i]; }
     q.k0 = (uint32_t)key; q.k1 = (uint32_t)(key >> 32); q.f = filter_index;
     q.flags = c->fast_ssa ? kChainFastSsa : 0u;
     HIP_TRY(hipMemcpyAsync(dcp, &q, sizeof q, hipMemcpyHostToDevice, c->stream));

@@ -77,9 +77,10 @@ struct ChainParam {
     double logp, log1mp;       // log(p), log1p(-p)  (host glibc, identical to the oracle's)
     uint32_t k0, k1;           // Philox key
     uint32_t f;                // filter index
-    uint32_t flags;            // kChainFastSsa: the SIR certified f32 event loop may run (EPIPF_SSA_FAST=0 clears it)
+    uint32_t flags;            // kChainFastSsa: the certified f32 event loop may run (EPIPF_SSA_FAST=0 clears it)
+    float thetaf[kMaxTheta];   // theta rounded to f32 on the host (scalar loads: the fast path's rates stay in SGPRs)
 };
-constexpr uint32_t kChainFastSsa = 1u;
+constexpr uint32_t kChainFastSsa = 1u;   // (all models)
 
 // ------------------------------------------------------------------------------- f64 log, table driven
 // log(x) for normal x > 0, within 1 ulp of glibc's correctly rounded log (exact near x = 1).  x = 2^k z with
@@ -354,81 +355,238 @@ struct SubgroupsState {                                                // gilles
 template <int G> struct SsaState<kSubgroups, G> : SubgroupsState<G> {};
 template <int G> struct SsaState<kSubgroups2, G> : SubgroupsState<G> {};
 
-// ------------------------------------------------------------------------------- SIR f32 fast path
+// ------------------------------------------------------------------------------- certified f32 fast path
 // The exact loop above spends ~45 f64 operations per event (the table log alone ~20, v_rcp_f64 16 cycles).
 // The fast path takes every decision in f32 and certifies it (derivation: DESIGN.md §4):
-//   channel  q = a0 * rcp(as) is within 2^-20 of the reference's ratio (a0: 3 roundings, as: 4, v_rcp_f32
-//            <= 1.53 ulp, product 1).  U lies in [uf, uf + 2^-23) for uf its top 23 bits; with uc = uf + 2^-24,
-//            the decision q_ref <= U is certain when |q - uc| > 2^-19, else sir_channel_exact decides.
-//   clock    time is kept in units of 1/ln 2 and counted down: rem = tmax/ln2 + sum(log2(x_f) * rcp(as)), the
-//            event is inside the step iff rem >= 0 (the exact path's t + tau <= tmax, scaled).  x_f = 1 - U from
-//            two converts (relative error <= 3 * 2^-24 for x >= 2^-20); v_log_f32 is within 2 ulp of |log2 x| on
-//            every float in [2^-20, 1), v_rcp_f32 within 1.53 ulp (exhaustive, scripts/f32_accuracy.hip).  Per
-//            event |tau2_f - tau2| <= 9.6*2^-24 |tau2_f| + 4.4*2^-24 rcp(as), so with R = sum rcp(as) the
-//            remaining time is within B = 11*2^-24 tmax/ln2 + 5*2^-24 R (float rounding of B and rem included)
-//            of the exact path's, scaled.  rem > B: the event is the exact path's; rem < -B: the step ends
-//            there, as in the exact path; otherwise (and for x < 2^-20, probability 2^-20 per event) the lane
-//            hands its whole step to the exact loop, from the untouched parent state.
-// Eligible lanes: N < 2^24 (counts exact in f32; at most 2N < 2^25 events per step) and beta/N, gamma zero or
-// in [2^-60, 2^40] / [2^-60, 2^60] (every f32 intermediate stays normal).
-constexpr float kChanBandF = 0x1.0p-19f;
-constexpr float kClockTmaxF = 11.0f * 0x1.0p-24f;
-constexpr float kClockRF = 5.0f * 0x1.0p-24f;
+//   channel  the cumulative propensities c_i and their total are f32 sums of positive terms with relative
+//            error <= e_as ulp (per model below); q_i = c_i * rcp(total) is then within e_q = 2 e_as + 5 ulp of
+//            the reference's ratio (v_rcp_f32 <= 1.53 ulp).  U lies in [uf, uf + 2^-23) for uf its top 23 bits;
+//            with uc = uf + 2^-24, every decision q_ref <= U is certain when all |q_i - uc| > kBand >= (e_q + 2)
+//            ulp, else the model's *_channel_exact evaluates the reference expression in f64.
+//   clock    time is kept in units of 1/ln 2 and counted down: rem = tmax/ln2 + sum(log2(x_f) * rcp(total)),
+//            the event is inside the step iff rem >= 0 (the exact path's t + tau <= tmax, scaled).  x_f = 1 - U
+//            from two converts (relative error <= 3 ulp for x >= 2^-20); v_log_f32 is within 2 ulp of |log2 x|
+//            on every float in [2^-20, 1) (exhaustive, scripts/f32_accuracy.hip).  Per event
+//            |tau2_f - tau2| <= (e_as + 5.5) ulp |tau2_f| + 4.4 ulp rcp(total), so with R = sum rcp(total) the
+//            remaining time is within B = kClockT tmax/ln2 + 5 ulp R of the exact path's, scaled
+//            (kClockT = e_as + 7 ulp covers the float evaluation of B and rem and at most 2^26 events).
+//            rem > B: the event is the exact path's; rem < -B: the step ends there, as in the exact path;
+//            otherwise (and for x < 2^-20, probability 2^-20 per event) the lane hands its whole step to the
+//            exact loop, from the untouched parent state.
+// Eligible lanes: population < 2^24 (counts exact in f32; < 2^26 events per step) and every rate parameter
+// zero or in [2^-60, 2^40] (every f32 intermediate stays normal).
+constexpr float kUlpF = 0x1.0p-24f;
+constexpr float kClockRF = 5.0f * kUlpF;
 constexpr double kInvLn2 = 0x1.71547652b82fep0;
 
-__device__ __forceinline__ bool sir_fast_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
-                                                   double tmax, int& nev_out, int& iters) {
-    const double N = (x[0] + x[1]) + x[2];
-    const float bN = (float)(cp.theta[0] / N), g = (float)cp.theta[1];
+__device__ __forceinline__ bool rate_ok(float v) { return v == 0.f || (v >= 0x1.0p-60f && v <= 0x1.0p40f); }
+
+template <int MODEL, int G>
+struct FastSsa;
+
+template <>
+struct FastSsa<kSIR, 1> {                                              // gillespie_algo.py:10-75
+    static constexpr int NCH = 2;
+    static constexpr float kBand = 0x1.0p-19f;                         // e_as = 4, e_q = 13
+    static constexpr float kClockT = 11.0f * kUlpF;
+    double N;
+    float S, I, bN, g, S0, SI0;
+    __device__ __forceinline__ bool load(const double* x, const ChainParam& cp) {
+        N = (x[0] + x[1]) + x[2];                                      // :35
+        bN = (float)(cp.theta[0] / N);
+        g = cp.thetaf[1];
+        S = S0 = (float)x[0];
+        I = (float)x[1];
+        SI0 = S + I;
+        return N < 16777216.0 && rate_ok(bN) && rate_ok(g);
+    }
+    __device__ __forceinline__ bool active() const { return I > 0.f; }   // :48
+    __device__ __forceinline__ float cum(float* c) const {             // :38-39
+        c[0] = bN * (S * I);
+        return fmaf(g, I, c[0]);
+    }
+    __device__ __forceinline__ int exact_channel(const ChainParam& cp, double u) const {
+        return sir_channel_exact(cp.theta[0], cp.theta[1], (double)S, (double)I, N, u) ? 1 : 0;
+    }
+    __device__ __forceinline__ void apply(int ch, float s) {           // s = +1 apply, -1 undo; :43-46
+        S = S - (ch == 0 ? s : 0.f);
+        I = I + (ch == 0 ? s : -s);
+    }
+    __device__ __forceinline__ int save(double* x) const {
+        const float inf = S0 - S, rec = SI0 - (S + I);
+        x[0] = (double)S; x[1] = (double)I; x[2] = x[2] + (double)rec;
+        return (int)(inf + rec);
+    }
+};
+
+template <>
+struct FastSsa<kSEIR, 1> {                                             // gillespie_algo.py:78-146
+    static constexpr int NCH = 3;
+    static constexpr float kBand = 0x1.0p-19f;                         // e_as = 5, e_q = 15
+    static constexpr float kClockT = 12.0f * kUlpF;
+    double N;
+    float S, E, I, bN, al, g, S0, I0, SEI0;
+    __device__ __forceinline__ bool load(const double* x, const ChainParam& cp) {
+        N = ((x[0] + x[1]) + x[2]) + x[3];                             // :104
+        bN = (float)(cp.theta[0] / N);
+        al = cp.thetaf[1];
+        g = cp.thetaf[2];
+        S = S0 = (float)x[0];
+        E = (float)x[1];
+        I = I0 = (float)x[2];
+        SEI0 = (S + E) + I;
+        return N < 16777216.0 && rate_ok(bN) && rate_ok(al) && rate_ok(g);
+    }
+    __device__ __forceinline__ bool active() const { return E > 0.f || I > 0.f; }   // :119
+    __device__ __forceinline__ float cum(float* c) const {             // :107-109
+        c[0] = bN * (S * I);
+        c[1] = fmaf(al, E, c[0]);
+        return fmaf(g, I, c[1]);
+    }
+    __device__ __forceinline__ int exact_channel(const ChainParam& cp, double u) const {
+        return seir_channel_exact(cp.theta[0], cp.theta[1], cp.theta[2], (double)S, (double)E, (double)I, N, u);
+    }
+    __device__ __forceinline__ void apply(int ch, float s) {           // :113-117
+        S = S - (ch == 0 ? s : 0.f);
+        E = E + (ch == 0 ? s : (ch == 1 ? -s : 0.f));
+        I = I + (ch == 1 ? s : (ch == 2 ? -s : 0.f));
+    }
+    __device__ __forceinline__ int save(double* x) const {
+        const float n0 = S0 - S, n2 = SEI0 - ((S + E) + I), n1 = (I - I0) + n2;
+        x[0] = (double)S; x[1] = (double)E; x[2] = (double)I; x[3] = x[3] + (double)n2;
+        return (int)((n0 + n1) + n2);
+    }
+};
+
+template <int G>
+struct FastSubgroups {                                                 // gillespie_algo.py:148-233
+    static constexpr int NCH = G * G + G;
+    static constexpr float kBand = (2 * (4 + NCH) + 7 <= 32) ? 0x1.0p-19f : 0x1.0p-18f;   // (e_q + 2) ulp
+    static constexpr float kClockT = (float)(NCH + 11) * kUlpF;        // e_as = 4 + NCH
+    double sumN;
+    float S[G], I[G], Ng[G], invN, S0sum, R0sum;
+    const float* b;                                                    // beta[G][G] then gamma, f32 (SGPRs)
+    __device__ __forceinline__ bool load(const double* x, const ChainParam& cp) {
+        sumN = 0.0;
+        bool ok = true;
+        S0sum = 0.f;
+        R0sum = 0.f;
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+            sumN = sumN + ((x[3 * q] + x[3 * q + 1]) + x[3 * q + 2]);  // sum(N), :176,:182
+            S[q] = (float)x[3 * q];
+            I[q] = (float)x[3 * q + 1];
+            Ng[q] = (S[q] + I[q]) + (float)x[3 * q + 2];
+            S0sum += S[q];
+            R0sum += (float)x[3 * q + 2];
+        }
+        b = cp.thetaf;
+#pragma unroll
+        for (int q = 0; q <= G * G; ++q) ok = ok && rate_ok(b[q]);
+        invN = (float)(1.0 / sumN);
+        return ok && sumN >= 1.0 && sumN < 16777216.0;
+    }
+    __device__ __forceinline__ bool active() const {                   // :192-193, :222
+        float inf = 0.f;
+#pragma unroll
+        for (int q = 0; q < G; ++q) inf += I[q];
+        return inf > 0.f;
+    }
+    __device__ __forceinline__ float cum(float* c) const {             // channel order, :180-185
+        float run = 0.f;
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+            const float cI = I[q] * invN;
+#pragma unroll
+            for (int q2 = 0; q2 < G; ++q2) {
+                run = fmaf(b[q * G + q2] * S[q2], cI, run);
+                if (q * (G + 1) + q2 < NCH - 1) c[q * (G + 1) + q2] = run;
+            }
+            run = fmaf(b[G * G], I[q], run);
+            if (q * (G + 1) + G < NCH - 1) c[q * (G + 1) + G] = run;
+        }
+        return run;
+    }
+    __device__ __forceinline__ int exact_channel(const ChainParam& cp, double u) const {
+        double Sd[G], Id[G];
+#pragma unroll
+        for (int q = 0; q < G; ++q) { Sd[q] = (double)S[q]; Id[q] = (double)I[q]; }
+        return subgroups_channel_exact<G>(cp.theta, Sd, Id, sumN, u);
+    }
+    __device__ __forceinline__ void apply(int ch, float s) {
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+#pragma unroll
+            for (int q2 = 0; q2 < G; ++q2)
+                if (ch == q * (G + 1) + q2) { S[q2] -= s; I[q2] += s; }        // s_{g}_{g2}: :183
+            if (ch == q * (G + 1) + G) I[q] -= s;                             // i_{g}: :185
+        }
+    }
+    __device__ __forceinline__ int save(double* x) const {
+        float inf = S0sum, rec = -R0sum;
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+            const float R = (Ng[q] - S[q]) - I[q];
+            inf -= S[q];
+            rec += R;
+            x[3 * q] = (double)S[q]; x[3 * q + 1] = (double)I[q]; x[3 * q + 2] = (double)R;
+        }
+        return (int)(inf + rec);
+    }
+};
+template <int G> struct FastSsa<kSubgroups, G> : FastSubgroups<G> {};
+template <int G> struct FastSsa<kSubgroups2, G> : FastSubgroups<G> {};
+
+template <int MODEL, int G>
+__device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
+                                               double tmax, int& nev_out, int& iters) {
+    using F = FastSsa<MODEL, G>;
+    constexpr int NCH = F::NCH;
     iters = 0;
     nev_out = 0;
     if (!(cp.flags & kChainFastSsa)) return false;
-    if (!(N < 16777216.0 && (bN == 0.f || (bN >= 0x1.0p-60f && bN <= 0x1.0p40f)) &&
-          (g == 0.f || (g >= 0x1.0p-60f && g <= 0x1.0p60f))))
-        return false;
-    const float S0 = (float)x[0], SI0 = (float)x[0] + (float)x[1];
-    float S = S0, I = (float)x[1];
+    F st;
+    if (!st.load(x, cp)) return false;
     double rem = tmax * kInvLn2;                                       // remaining time, units of 1/ln 2
-    const float Bt = (float)rem * kClockTmaxF;
+    const float Bt = (float)rem * F::kClockT;
     float R = 0.f, df = 0.f, B = 0.f;
     uint32_t ks = 0;                                                   // event index, wave-uniform (SGPR)
-    bool alive = I > 0.f, ok = true, tiny = false, second = false;
+    bool alive = st.active(), ok = true, tiny = false;
+    int ch = 0;
     Block rn{0u, 0u, 0u, 0u};
     if (alive) rn = philox<true>(0u, j, ptag, cp.f, cp.k0, cp.k1);    // x word inverted: ~x
     while (alive) {
         const Block r = rn;
         ks = __builtin_amdgcn_readfirstlane(ks) + 1u;
         rn = philox<true>(ks, j, ptag, cp.f, cp.k0, cp.k1);
-        const float a0 = bN * (S * I);                                 // gillespie_algo.py:38
-        const float as = fmaf(g, I, a0);                               // :39, :62
-        const float ri = __builtin_amdgcn_rcpf(as);
-        const float q = a0 * ri;
-        const float uc = __uint_as_float(0x3F800000u | (r.w >> 9)) - (1.0f - 0x1.0p-24f);   // uf + 2^-24
-        second = q < uc;                                               // choice(2, p=a/sum(a)), :63
-        if (fabsf(q - uc) <= kChanBandF)
-            second = sir_channel_exact(cp.theta[0], cp.theta[1], (double)S, (double)I, N, u01(r.z, r.w));
+        float c[NCH - 1];
+        const float ri = __builtin_amdgcn_rcpf(st.cum(c));
+        const float uc = __uint_as_float(0x3F800000u | (r.w >> 9)) - (1.0f - kUlpF);   // uf + 2^-24
+        bool close = false;
+        ch = 0;
+#pragma unroll
+        for (int i = 0; i < NCH - 1; ++i) {                            // numpy choice, searchsorted right
+            const float q = c[i] * ri;
+            ch += (q < uc) ? 1 : 0;
+            close |= fabsf(q - uc) <= F::kBand;
+        }
+        if (close) ch = st.exact_channel(cp, u01(r.z, r.w));
         const uint32_t nh = ~r.y;
         const float xf = fmaf((float)nh, 0x1.0p-32f, (float)r.x * 0x1.0p-64f);     // 1 - U (r.x is ~x)
-        rem = rem + (double)(__builtin_amdgcn_logf(xf) * ri);          // exponential, :62
+        rem = rem + (double)(__builtin_amdgcn_logf(xf) * ri);          // np.random.exponential
         R += ri;
         df = (float)rem;
         B = fmaf(R, kClockRF, Bt);
         tiny = nh < 4096u;
-        ok = df > B && !tiny;                                          // certainly inside the step, :65-66
-        S = S - (second ? 0.f : 1.f);                                  // applied unconditionally; a lane that
-        I = I + (second ? -1.f : 1.f);                                 // fails `ok` leaves and undoes it below
-        alive = ok && I > 0.f;
+        ok = df > B && !tiny;                                          // certainly inside the step
+        st.apply(ch, 1.f);                                             // undone below if the lane overshoots
+        alive = ok && st.active();
     }
     if (!ok) {
         if (tiny || !(df < -B)) return false;                         // boundary too close to call: exact loop
-        S = S + (second ? 0.f : 1.f);                                  // the overshooting event is not applied
-        I = I - (second ? -1.f : 1.f);
+        st.apply(ch, -1.f);                                            // the overshooting event is not applied
     }
-    const float infections = S0 - S, recoveries = SI0 - (S + I);
-    x[0] = (double)S;
-    x[1] = (double)I;
-    x[2] = x[2] + (double)recoveries;
-    nev_out = (int)(infections + recoveries);
+    nev_out = st.save(x);
     iters = nev_out + (ok ? 0 : 1);
     return true;
 }
@@ -436,20 +594,17 @@ __device__ __forceinline__ bool sir_fast_propagate(double* x, const ChainParam& 
 // One particle over [0, tmax] (every lane of the wave starts together, so the event index k is wave-uniform).
 // Software pipelining: event k+1's Philox block (counter-based, so independent of event k's outcome) is
 // computed while event k's f64 work runs, which gives each wave two independent dependency chains.  The
-// block drawn after the last event is discarded (one per particle-step).  SIR lanes first try the certified
-// f32 path; lanes it cannot certify run this exact loop from the untouched parent state.
+// block drawn after the last event is discarded (one per particle-step).  Lanes first try the certified f32
+// path; lanes it cannot certify run this exact loop from the untouched parent state.
 template <int MODEL, int G>
 __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
                                              double tmax, const LogTab* __restrict__ tab, int& iters, int& exact) {
-    int fast_iters = 0;
+    int fast_iters = 0, fast_nev = 0;
     exact = 1;
-    if constexpr (MODEL == kSIR) {
-        int nev = 0;
-        if (sir_fast_propagate(x, cp, j, ptag, tmax, nev, fast_iters)) {
-            iters = fast_iters;
-            exact = 0;
-            return nev;
-        }
+    if (fast_propagate<MODEL, G>(x, cp, j, ptag, tmax, fast_nev, fast_iters)) {
+        iters = fast_iters;
+        exact = 0;
+        return fast_nev;
     }
     SsaState<MODEL, G> st;
     st.load(x, cp);

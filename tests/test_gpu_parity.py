@@ -299,14 +299,14 @@ def test_full_size_cfg2_properties(datasets_golden):
     np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-8)
 
 
-def _engine_with_fast_ssa(enabled, N, T, chains):
-    """A fresh context with the certified f32 SIR event loop on or off (EPIPF_SSA_FAST is read at create)."""
+def _engine_with_fast_ssa(enabled, N, T, chains, model="sir", groups=1):
+    """A fresh context with the certified f32 event loop on or off (EPIPF_SSA_FAST is read at create)."""
     import os
     from epipf.engine import Engine
     old = os.environ.get("EPIPF_SSA_FAST")
     os.environ["EPIPF_SSA_FAST"] = "1" if enabled else "0"
     try:
-        return Engine("sir", 1, N, T, chains)
+        return Engine(model, groups, N, T, chains)
     finally:
         if old is None:
             del os.environ["EPIPF_SSA_FAST"]
@@ -355,3 +355,34 @@ def test_fast_ssa_simulate_equals_exact_path():
             eng.close()
         np.testing.assert_array_equal(res[0][0], res[1][0])
         assert res[0][1] == res[1][1]
+
+
+@pytest.mark.parametrize("model,groups,ds,theta,npop,mu,obs", [
+    ("seir", 1, "cfg3_noisy", [[0.5, 0.2, 0.1], [0.7, 0.3, 0.15], [0.4, 0.25, 0.05], [0.5, 0.2, 0.1]], 10000.0,
+     20.0, True),
+    ("sir_subgroups", 2, "sub_binom", [[5, 2, 1, 3, 0.5], [4, 1, 1, 4, 1.0], [6, 2.5, 1.5, 3, 0.6],
+                                       [5, 2, 1, 3, 0.5]], [2030.0, 3040.0], [30.0, 40.0], False),
+    ("sir_subgroups2", 2, "sub2_binom", [[5, 2, 1, 3, 0.5], [4, 1, 1, 4, 1.0], [6, 2.5, 1.5, 3, 0.6],
+                                         [5, 2, 1, 3, 0.5]], [2030.0, 3040.0], [30.0, 40.0], False),
+])
+def test_fast_ssa_path_equals_exact_path_other_models(datasets_golden, model, groups, ds, theta, npop, mu, obs):
+    """SEIR and two-group filters at N = 5000: certified f32 loop and f64 loop give identical bits."""
+    Y = datasets_golden[ds]
+    T, N, C = Y.shape[0], 5000, len(theta)
+    th = np.array(theta, dtype=np.float64)
+    out = []
+    for fast in (True, False):
+        eng = _engine_with_fast_ssa(fast, N, T, C, model, groups)
+        eng.set_observations(Y)
+        eng.set_population(npop, mu)
+        eng.set_profiling(2)
+        lz, st = eng.run(th, [0.1] * C, [21 + c for c in range(C)], [5] * C, observations=obs)
+        hid, anc = eng.history(C)
+        out.append((lz, st, hid, anc, eng.stats()))
+        eng.close()
+    (lz1, st1, h1, a1, s1), (lz0, st0, h0, a0, s0) = out
+    np.testing.assert_array_equal(st1, st0)
+    np.testing.assert_array_equal(h1, h0)
+    np.testing.assert_array_equal(a1, a0)
+    np.testing.assert_array_equal(lz1, lz0)
+    assert s1["events"] == s0["events"] and s1["ssa_exact_lanes"] < s0["ssa_exact_lanes"]
