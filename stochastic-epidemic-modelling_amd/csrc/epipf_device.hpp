@@ -362,7 +362,9 @@ template <int G> struct SsaState<kSubgroups2, G> : SubgroupsState<G> {};
 //            error <= e_as ulp (per model below); q_i = c_i * rcp(total) is then within e_q = 2 e_as + 5 ulp of
 //            the reference's ratio (v_rcp_f32 <= 1.53 ulp).  U lies in [uf, uf + 2^-23) for uf its top 23 bits;
 //            with uc = uf + 2^-24, every decision q_ref <= U is certain when all |q_i - uc| > kBand >= (e_q + 2)
-//            ulp, else the model's *_channel_exact evaluates the reference expression in f64.
+//            ulp, else the model's *_channel_exact evaluates the reference expression in f64.  Models with more
+//            than 3 channels compare c_i against T = uc * total with the band scaled by total (the reciprocal's
+//            error drops out: 2 e_as + 2 ulp, inside the same band).
 //   clock    time is kept in units of 1/ln 2 and counted down: rem = tmax/ln2 + sum(log2(x_f) * rcp(total)),
 //            the event is inside the step iff rem >= 0 (the exact path's t + tau <= tmax, scaled).  x_f = 1 - U
 //            from two converts (relative error <= 3 ulp for x >= 2^-20); v_log_f32 is within 2 ulp of |log2 x|
@@ -560,15 +562,25 @@ __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, 
         ks = __builtin_amdgcn_readfirstlane(ks) + 1u;
         rn = philox<true>(ks, j, ptag, cp.f, cp.k0, cp.k1);
         float c[NCH - 1];
-        const float ri = __builtin_amdgcn_rcpf(st.cum(c));
+        const float total = st.cum(c);
+        const float ri = __builtin_amdgcn_rcpf(total);
         const float uc = __uint_as_float(0x3F800000u | (r.w >> 9)) - (1.0f - kUlpF);   // uf + 2^-24
         bool close = false;
         ch = 0;
+        if constexpr (NCH <= 3) {                                      // ratios q_i = c_i / total
 #pragma unroll
-        for (int i = 0; i < NCH - 1; ++i) {                            // numpy choice, searchsorted right
-            const float q = c[i] * ri;
-            ch += (q < uc) ? 1 : 0;
-            close |= fabsf(q - uc) <= F::kBand;
+            for (int i = 0; i < NCH - 1; ++i) {                        // numpy choice, searchsorted right
+                const float q = c[i] * ri;
+                ch += (q < uc) ? 1 : 0;
+                close |= fabsf(q - uc) <= F::kBand;
+            }
+        } else {                                                       // c_i against uc * total: one multiply
+            const float T = uc * total, band = F::kBand * total;       // per draw instead of one per channel
+#pragma unroll
+            for (int i = 0; i < NCH - 1; ++i) {
+                ch += (c[i] < T) ? 1 : 0;
+                close |= fabsf(c[i] - T) <= band;
+            }
         }
         if (close) ch = st.exact_channel(cp, u01(r.z, r.w));
         const uint32_t nh = ~r.y;
