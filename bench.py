@@ -153,9 +153,15 @@ def main():
     value = filters_all * N * T / dt
 
     # roofline of the dominant kernel: pf_step_kernel (resample + gather + SSA + weight + in-block scan)
-    launches = max(1, st["step_launches"])
-    avg_launch_s = st["step_ms"] / 1e3 / launches
-    units_per_launch = filters * N / args.steps                      # particle-steps per launch (all chains)
+    # One filter step of every chain on this rank is issued as `streams` concurrent pf_step_kernel launches, one
+    # per chain group on its own stream.  The roofline is per kernel launch, as rocprofv3 sees it:
+    # HIP events on each group's stream span its back-to-back step kernels (launch-to-completion, so a kernel
+    # waiting for CUs held by the other groups counts; rocprofv3's durations do not); the step wall time too.
+    streams = max(1, min(int(os.environ.get("EPIPF_STREAMS", 4)), C))
+    launches = max(1, st["step_kernel_launches"])
+    avg_launch_s = st["step_kernel_ms"] / 1e3 / launches
+    step_wall_s = st["step_ms"] / 1e3 / max(1, st["step_launches"])
+    units_per_launch = filters * N / args.steps / streams            # particle-steps per kernel launch
     n_comp = {"sir": 3, "seir": 4}.get(meta["model"], 3 * len(np.atleast_1d(meta["n_population"])))
     bytes_per_unit = 8 * n_comp + 40                                  # 8C+40 B per particle-step
     achieved = units_per_launch * bytes_per_unit / avg_launch_s / 1e9
@@ -163,7 +169,8 @@ def main():
     pmc_path = os.path.join(REPO, "profiles", "pmc_step_kernel.json")
     if os.path.exists(pmc_path):
         try:
-            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+            per_unit = json.load(open(pmc_path)).get("hbm_bytes_per_particle_step")
+            traffic = per_unit * units_per_launch if per_unit else None
         except (OSError, ValueError):
             traffic = None
     events_per_s = cst["events"] / (cst["step_ms"] / 1e3) if cst["step_ms"] > 0 else None
@@ -209,7 +216,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "pf_step_kernel", "avg_launch_us": avg_launch_s * 1e6,
-                         "bytes_per_particle_step": bytes_per_unit, "particle_steps_per_launch": units_per_launch},
+                         "bytes_per_particle_step": bytes_per_unit, "particle_steps_per_launch": units_per_launch,
+                         "concurrent_launches_per_step": streams, "step_wall_us": step_wall_s * 1e6},
             "events_per_s": events_per_s,
             "ssa_lane_utilisation": lane_use,
             "resample_fallbacks": st["resample_fallbacks"],

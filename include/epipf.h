@@ -84,6 +84,10 @@ typedef struct {
     int64_t abc_trials;          /* ABC trials simulated (accepted or not) */
     int64_t ssa_exact_lanes;     /* filter particle-steps simulated on the exact f64 SSA loop (profiling counters) */
     int64_t ssa_exact_waves;     /* filter wave-steps with at least one such particle-step */
+    double step_kernel_ms;       /* summed span of each chain group's back-to-back step kernels, HIP events on the
+                                    group's own stream (profiling on) */
+    int64_t step_kernel_launches;/* their number: one step of all chains (step_ms) is one launch per chain group on
+                                    concurrent streams (EPIPF_STREAMS, default 4) */
 } epipf_stats;
 
 /* groups: G for the subgroup models (1 <= G <= 4), ignored (1) for SIR/SEIR.

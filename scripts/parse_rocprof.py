@@ -54,6 +54,11 @@ def main(d):
         raw = (avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024.0
         out["hbm_bytes_per_launch"] = raw
         out["hbm_bytes_per_launch_read_doubled"] = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024.0
+        # per particle-step (one lane per particle): launches of chain groups on concurrent streams have
+        # different grid sizes than a one-launch-per-step run, so bench.py scales this figure instead
+        lanes = float(meta.get("Grid_Size") or 0)
+        if lanes > 0:
+            out["hbm_bytes_per_particle_step"] = raw / lanes
     print(json.dumps(out, indent=1))
     with open(os.path.join(d, "pmc_step_kernel.json"), "w") as f:
         json.dump(out, f, indent=1)

@@ -93,6 +93,13 @@ struct epipf_ctx {
     void* abc = nullptr;
     bool abc_order = true;   // length-ordered ABC lanes (EPIPF_ABC_ORDER=0 disables)
     bool fast_ssa = true;    // certified f32 event loop (EPIPF_SSA_FAST=0 disables; results are identical)
+    int n_streams = kMaxFilterStreams;   // chain groups on concurrent streams (EPIPF_STREAMS overrides, 1..4)
+    hipStream_t aux[kMaxFilterStreams] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t join[kMaxFilterStreams] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t fork = nullptr;
+    hipEvent_t gb[kMaxFilterStreams] = {nullptr, nullptr, nullptr, nullptr};   // per-group step spans (timing)
+    hipEvent_t ge[kMaxFilterStreams] = {nullptr, nullptr, nullptr, nullptr};
+    int last_groups = 1;
 };
 
 // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp): D bounds the depth of the parallel
@@ -119,6 +126,15 @@ static void free_ctx(epipf_ctx* c) {
         if (p) (void)hipHostFree(p);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->join)
+        if (e) (void)hipEventDestroy(e);
+    for (int g = 0; g < kMaxFilterStreams; ++g) {
+        if (c->gb[g]) (void)hipEventDestroy(c->gb[g]);
+        if (c->ge[g]) (void)hipEventDestroy(c->ge[g]);
+    }
+    if (c->fork) (void)hipEventDestroy(c->fork);
+    for (auto& st : c->aux)
+        if (st) { (void)hipStreamSynchronize(st); (void)hipStreamDestroy(st); }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -154,6 +170,7 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     c->max_chains = max_chains;
     c->wg = default_wg(n_particles);
     if (const char* e = getenv("EPIPF_SSA_FAST")) c->fast_ssa = atoi(e) != 0;
+    if (const char* e = getenv("EPIPF_STREAMS")) c->n_streams = std::max(1, std::min(kMaxFilterStreams, atoi(e)));
     c->B = (n_particles + c->wg - 1) / c->wg;
     if (step_lds_bytes(c->B, c->wg) > 160 * 1024) {
         free_ctx(c);
@@ -191,6 +208,21 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     }
     for (auto& e : c->ev)
         if (hipEventCreate(&e) != hipSuccess) { free_ctx(c); return fail(EPIPF_EHIP, "hipEventCreate failed"); }
+    if (hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess) {
+        free_ctx(c);
+        return fail(EPIPF_EHIP, "hipEventCreate failed");
+    }
+    for (int g = 0; g < c->n_streams; ++g)
+        if (hipEventCreate(&c->gb[g]) != hipSuccess || hipEventCreate(&c->ge[g]) != hipSuccess) {
+            free_ctx(c);
+            return fail(EPIPF_EHIP, "hipEventCreate failed");
+        }
+    for (int g = 1; g < c->n_streams; ++g)
+        if (hipStreamCreateWithFlags(&c->aux[g], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->join[g], hipEventDisableTiming) != hipSuccess) {
+            free_ctx(c);
+            return fail(EPIPF_EHIP, "auxiliary stream creation failed");
+        }
     if (launch_log_table(c->logtab, c->stream) != hipSuccess ||
         hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
@@ -296,9 +328,24 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     a.counters = c->counters;
     for (int g = 0; g < kMaxG; ++g) { a.npop[g] = c->npop[g]; a.mu[g] = c->mu[g]; a.emu[g] = c->emu[g]; a.kmax[g] = c->kmax[g]; }
 
-    hipEvent_t e0 = c->profiling ? c->ev[0] : nullptr, e1 = c->profiling ? c->ev[1] : nullptr,
-               e2 = c->profiling ? c->ev[2] : nullptr;
-    hipError_t le = launch_filter(a, c->model, c->G, obs_model, n_chains, c->stream, e0, e1, e2);
+    FilterStreams fs{};
+    fs.n = std::min(c->n_streams, n_chains);
+    fs.s[0] = c->stream;
+    if (fs.n > 1) HIP_TRY(hipEventRecord(c->fork, c->stream));    // the groups' inputs are on c->stream
+    for (int g = 1; g < fs.n; ++g) {
+        fs.s[g] = c->aux[g];
+        fs.join[g] = c->join[g];
+        HIP_TRY(hipStreamWaitEvent(c->aux[g], c->fork, 0));
+    }
+    fs.ev_init = c->profiling ? c->ev[0] : nullptr;
+    fs.ev_step0 = c->profiling ? c->ev[1] : nullptr;
+    fs.ev_end = c->profiling ? c->ev[2] : nullptr;
+    for (int g = 0; g < fs.n; ++g) {
+        fs.g_begin[g] = c->profiling ? c->gb[g] : nullptr;
+        fs.g_end[g] = c->profiling ? c->ge[g] : nullptr;
+    }
+    c->last_groups = fs.n;
+    hipError_t le = launch_filter(a, c->model, c->G, obs_model, n_chains, fs);
     if (le != hipSuccess) return fail(EPIPF_EHIP, "kernel launch failed: %s", hipGetErrorString(le));
     HIP_TRY(hipMemcpyAsync(c->h_status, c->status, sizeof(int32_t) * n_chains, hipMemcpyDeviceToHost, c->stream));
     if (log_zetas_out)
@@ -329,6 +376,12 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
         c->stats.init_launches += 1;
         c->stats.step_ms += ms_step;
         c->stats.step_launches += c->T - 1;
+        for (int g = 0; g < c->last_groups; ++g) {        // each group's back-to-back step kernels on its stream
+            float ms_g = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms_g, c->gb[g], c->ge[g]));
+            c->stats.step_kernel_ms += ms_g;
+            c->stats.step_kernel_launches += c->T - 1;
+        }
     }
     unsigned long long tot[kNumCounters] = {0, 0, 0, 0, 0, 0};
     for (int sl = 0; sl < kCounterSlots; ++sl)

@@ -27,6 +27,7 @@ __device__ __forceinline__ unsigned long long* counter_slot(unsigned long long* 
 //   Y        f64   [T][K];  lf f64 [lf_max+1] = lgamma(n+1)
 struct StepArgs {
     int N, T, B, wg, max_chains, resample_mode, count_events, lf_max;
+    int chain0;                   // first chain of this launch (chain groups run on separate streams)
     size_t hist_stride, anc_stride, wstride, bstride;
     double cert_k;                // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp)
     const double* Y;
@@ -122,9 +123,19 @@ struct AbcGatherArgs {
     double* theta_out;           // [samples][2]
 };
 
+// Streams of one filter run: group g of the chains runs on s[g]; s[0] is the context stream, the others have
+// waited for its inputs.  join[g] (g > 0) is recorded at the end of group g, and s[0] waits for all of them.
+constexpr int kMaxFilterStreams = 4;
+struct FilterStreams {
+    int n;
+    hipStream_t s[kMaxFilterStreams];
+    hipEvent_t join[kMaxFilterStreams];
+    hipEvent_t ev_init, ev_step0, ev_end;   // timing (profiling on) or null
+    hipEvent_t g_begin[kMaxFilterStreams], g_end[kMaxFilterStreams];   // per-group step-kernel span, or null
+};
+
 size_t step_lds_bytes(int B, int wg);
-hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, hipStream_t s,
-                         hipEvent_t ev_init, hipEvent_t ev_step0, hipEvent_t ev_end);
+hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, const FilterStreams& fs);
 hipError_t launch_path_sample(const PathArgs& a, hipStream_t s);
 hipError_t launch_log_table(LogTab* tab, hipStream_t s);
 hipError_t launch_simulate(const SimArgs& a, int model, int G, hipStream_t s);

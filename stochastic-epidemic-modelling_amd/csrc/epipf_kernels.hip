@@ -12,6 +12,8 @@
 // produced the states, and the next launch only reads them.  The init kernel draws the Poisson initial
 // states (pmcmc.py:156-175) and the first weights.
 #include "epipf_device.hpp"
+#include <algorithm>
+
 #include "epipf_internal.hpp"
 
 namespace epipf {
@@ -48,7 +50,7 @@ __global__ __launch_bounds__(WG) void pf_init_kernel(StepArgs a) {
     using Sh = Shape<MODEL, G>;
     constexpr int C = Sh::C;
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int chain = blockIdx.y;
+    const int chain = a.chain0 + (int)blockIdx.y;
     const int j = blockIdx.x * WG + threadIdx.x;
     if (a.status[chain] != 0) return;
     const ChainParam cp = a.cp[chain];
@@ -95,7 +97,7 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
     double* red = smem + 2 * kLogTabEntries;             // WG/64 (+pad)
     double* bsum = red + 16;                             // B
     double* bpex = bsum + a.B;                           // B + WG
-    const int chain = blockIdx.y;
+    const int chain = a.chain0 + (int)blockIdx.y;
     const int tid = threadIdx.x;
     const int j = blockIdx.x * WG + tid;
     if (a.status[chain] != 0) return;
@@ -269,56 +271,65 @@ size_t step_lds_bytes(int B, int wg) {
 }
 
 template <int MODEL, int G, int OBS, int WG>
-static hipError_t launch_filter_t(const StepArgs& a, int n_chains, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
-                                  hipEvent_t ev2) {
-    const dim3 grid(a.B, n_chains), block(WG);
+static hipError_t launch_filter_t(const StepArgs& a, int n_chains, const FilterStreams& fs) {
+    // Chains are independent, so chain groups advance through their T steps on separate streams: one group's
+    // end-of-launch tail (the last, partial round of waves) overlaps the other groups' launches.
     const size_t lds = step_lds_bytes(a.B, WG);
-    if (ev0) (void)hipEventRecord(ev0, s);
-    hipLaunchKernelGGL((pf_init_kernel<MODEL, G, OBS, WG>), grid, block, lds, s, a);
-    if (ev1) (void)hipEventRecord(ev1, s);
-    for (int p = 1; p < a.T; ++p)
-        hipLaunchKernelGGL((pf_step_kernel<MODEL, G, OBS, WG>), grid, block, lds, s, a, p);
-    if (ev2) (void)hipEventRecord(ev2, s);
+    const int S = std::max(1, std::min(fs.n, n_chains));
+    for (int g = 0; g < S; ++g) {
+        StepArgs ag = a;
+        ag.chain0 = (int)((long)n_chains * g / S);
+        const int n_g = (int)((long)n_chains * (g + 1) / S) - ag.chain0;
+        const hipStream_t s = fs.s[g];
+        const dim3 grid(a.B, n_g), block(WG);
+        if (g == 0 && fs.ev_init) (void)hipEventRecord(fs.ev_init, s);
+        hipLaunchKernelGGL((pf_init_kernel<MODEL, G, OBS, WG>), grid, block, lds, s, ag);
+        if (g == 0 && fs.ev_step0) (void)hipEventRecord(fs.ev_step0, s);
+        if (fs.g_begin[g]) (void)hipEventRecord(fs.g_begin[g], s);
+        for (int p = 1; p < a.T; ++p)
+            hipLaunchKernelGGL((pf_step_kernel<MODEL, G, OBS, WG>), grid, block, lds, s, ag, p);
+        if (fs.g_end[g]) (void)hipEventRecord(fs.g_end[g], s);
+        if (g > 0) (void)hipEventRecord(fs.join[g], s);
+    }
+    for (int g = 1; g < S; ++g) (void)hipStreamWaitEvent(fs.s[0], fs.join[g], 0);
+    if (fs.ev_end) (void)hipEventRecord(fs.ev_end, fs.s[0]);
     return hipGetLastError();
 }
 
 template <int MODEL, int G, int WG>
-static hipError_t launch_obs(const StepArgs& a, int obs, int n_chains, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
-                             hipEvent_t e2) {
-    return obs == kBinomial ? launch_filter_t<MODEL, G, kBinomial, WG>(a, n_chains, s, e0, e1, e2)
-                            : launch_filter_t<MODEL, G, kNormal, WG>(a, n_chains, s, e0, e1, e2);
+static hipError_t launch_obs(const StepArgs& a, int obs, int n_chains, const FilterStreams& fs) {
+    return obs == kBinomial ? launch_filter_t<MODEL, G, kBinomial, WG>(a, n_chains, fs)
+                            : launch_filter_t<MODEL, G, kNormal, WG>(a, n_chains, fs);
 }
 
 template <int WG>
-static hipError_t launch_model(const StepArgs& a, int model, int G, int obs, int n_chains, hipStream_t s,
-                               hipEvent_t e0, hipEvent_t e1, hipEvent_t e2) {
+static hipError_t launch_model(const StepArgs& a, int model, int G, int obs, int n_chains, const FilterStreams& fs) {
     switch (model) {
-        case kSIR: return launch_obs<kSIR, 1, WG>(a, obs, n_chains, s, e0, e1, e2);
-        case kSEIR: return launch_obs<kSEIR, 1, WG>(a, obs, n_chains, s, e0, e1, e2);
+        case kSIR: return launch_obs<kSIR, 1, WG>(a, obs, n_chains, fs);
+        case kSEIR: return launch_obs<kSEIR, 1, WG>(a, obs, n_chains, fs);
         case kSubgroups:
             switch (G) {
-                case 1: return launch_obs<kSubgroups, 1, WG>(a, obs, n_chains, s, e0, e1, e2);
-                case 2: return launch_obs<kSubgroups, 2, WG>(a, obs, n_chains, s, e0, e1, e2);
-                case 3: return launch_obs<kSubgroups, 3, WG>(a, obs, n_chains, s, e0, e1, e2);
-                case 4: return launch_obs<kSubgroups, 4, WG>(a, obs, n_chains, s, e0, e1, e2);
+                case 1: return launch_obs<kSubgroups, 1, WG>(a, obs, n_chains, fs);
+                case 2: return launch_obs<kSubgroups, 2, WG>(a, obs, n_chains, fs);
+                case 3: return launch_obs<kSubgroups, 3, WG>(a, obs, n_chains, fs);
+                case 4: return launch_obs<kSubgroups, 4, WG>(a, obs, n_chains, fs);
             }
             break;
         case kSubgroups2:
             switch (G) {
-                case 1: return launch_obs<kSubgroups2, 1, WG>(a, obs, n_chains, s, e0, e1, e2);
-                case 2: return launch_obs<kSubgroups2, 2, WG>(a, obs, n_chains, s, e0, e1, e2);
-                case 3: return launch_obs<kSubgroups2, 3, WG>(a, obs, n_chains, s, e0, e1, e2);
-                case 4: return launch_obs<kSubgroups2, 4, WG>(a, obs, n_chains, s, e0, e1, e2);
+                case 1: return launch_obs<kSubgroups2, 1, WG>(a, obs, n_chains, fs);
+                case 2: return launch_obs<kSubgroups2, 2, WG>(a, obs, n_chains, fs);
+                case 3: return launch_obs<kSubgroups2, 3, WG>(a, obs, n_chains, fs);
+                case 4: return launch_obs<kSubgroups2, 4, WG>(a, obs, n_chains, fs);
             }
             break;
     }
     return hipErrorInvalidValue;
 }
 
-hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, hipStream_t s,
-                         hipEvent_t ev_init, hipEvent_t ev_step0, hipEvent_t ev_end) {
-    if (a.wg == 64) return launch_model<64>(a, model, G, obs, n_chains, s, ev_init, ev_step0, ev_end);
-    return launch_model<256>(a, model, G, obs, n_chains, s, ev_init, ev_step0, ev_end);
+hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, const FilterStreams& fs) {
+    if (a.wg == 64) return launch_model<64>(a, model, G, obs, n_chains, fs);
+    return launch_model<256>(a, model, G, obs, n_chains, fs);
 }
 
 hipError_t launch_log_table(LogTab* tab, hipStream_t s) {

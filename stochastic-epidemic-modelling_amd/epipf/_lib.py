@@ -43,6 +43,8 @@ class Stats(ctypes.Structure):
         ("abc_trials", ctypes.c_int64),
         ("ssa_exact_lanes", ctypes.c_int64),
         ("ssa_exact_waves", ctypes.c_int64),
+        ("step_kernel_ms", ctypes.c_double),
+        ("step_kernel_launches", ctypes.c_int64),
     ]
 
     def as_dict(self):
