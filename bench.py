@@ -39,7 +39,10 @@ def parse():
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--single-chain", action="store_true", help="also time 1 chain/GPU (extra field)")
+    ap.add_argument("--single-chain", action="store_true",
+                    help="also time 1 chain/GPU: one filter per MH iteration, and speculative MH (extra fields)")
+    ap.add_argument("--prefetch", type=int, default=32, help="filter slots per round of the speculative single chain")
+    ap.add_argument("--prefetch-iters", type=int, default=60, help="MH iterations timed for the speculative chain")
     return ap.parse_args()
 
 
@@ -176,7 +179,7 @@ def main():
     events_per_s = cst["events"] / (cst["step_ms"] / 1e3) if cst["step_ms"] > 0 else None
     lane_use = cst["lane_iterations"] / cst["wave_lane_slots"] if cst["wave_lane_slots"] else None
 
-    single = None
+    single = prefetch = None
     if args.single_chain and rank == 0 and world == 1:
         s1 = ChainSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=args.steps + 2, probs=meta["probs"],
                           observations=meta.get("observations", False),
@@ -190,6 +193,30 @@ def main():
         f1 = sum(s1.step() for _ in range(args.steps))
         torch.cuda.synchronize()
         single = f1 * N * T / (time.perf_counter() - t1)
+        # the same chain with prefetching (epipf.prefetch): speculative filters of future iterations share one
+        # batched launch sequence; only filters on the realised path count
+        from epipf.prefetch import PrefetchSampler
+        s2 = PrefetchSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=args.prefetch_iters + 40,
+                             probs=meta["probs"], observations=meta.get("observations", False), n_particles=N,
+                             n_population=meta["n_population"], mu=meta["mu"],
+                             rngs=[np.random.RandomState(args.seed)], keys=[chain_key(args.seed, 0)], device=local,
+                             mh_ratio="log", slots=args.prefetch)
+        s2.initialise()
+        while s2.i < 20:
+            s2.advance()
+        torch.cuda.synchronize()
+        i0, f0, r0, sp0 = s2.i, s2.filters_run[0], s2.rounds, s2.speculative_filters
+        t2 = time.perf_counter()
+        while s2.i < i0 + args.prefetch_iters:
+            s2.advance()
+        torch.cuda.synchronize()
+        dt2 = time.perf_counter() - t2
+        prefetch = {"value": (s2.filters_run[0] - f0) * N * T / dt2, "slots": args.prefetch,
+                    "iterations": s2.i - i0, "rounds": s2.rounds - r0,
+                    "iterations_per_round": (s2.i - i0) / max(1, s2.rounds - r0),
+                    "filters_evaluated": s2.speculative_filters - sp0,
+                    "acceptance_rate": (s2.acceptances[0] - 1) / max(1, s2.filters_run[0]),
+                    "ms_per_iteration": dt2 * 1e3 / max(1, s2.i - i0)}
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -230,6 +257,8 @@ def main():
         }
         if single is not None:
             line["single_chain_value"] = single
+        if prefetch is not None:
+            line["single_chain_prefetch"] = prefetch
         if base is not None:
             line["speedup_vs_cpu_baseline"] = value / base["value"]
         print(json.dumps(line), flush=True)

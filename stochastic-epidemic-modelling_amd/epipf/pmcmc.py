@@ -173,7 +173,7 @@ class ChainSampler:
 
     def __init__(self, Y, type_model, parameters, h, adaptive=False, sigma=None, iters=1000, observations=False,
                  probs=.1, n_particles=1000, n_population=4820, mu=20, *, rngs, keys, device=0,
-                 mh_ratio="reference", resample="multinomial", filter_index_start=0):
+                 mh_ratio="reference", resample="multinomial", filter_index_start=0, engine_chains=0):
         self.rngs = list(rngs)
         self.keys = np.asarray(keys, dtype=np.uint64)
         nc = self.nc = len(self.rngs)
@@ -193,7 +193,7 @@ class ChainSampler:
         Cc = n_compartments(mid, G)
         npop, mus = _population(mid, G, n_population, mu)
         self.iters = int(iters)
-        eng = self.eng = get_engine(mid, G, n_particles, T, nc, device)
+        eng = self.eng = get_engine(mid, G, n_particles, T, max(nc, int(engine_chains)), device)
         eng.set_observations(Y)
         eng.set_population(npop, mus)
         self.thetas = np.zeros((nc, self.iters, d))
@@ -344,34 +344,44 @@ class ChainSampler:
 def particle_mcmc_chains(Y, type_model, parameters, h, adaptive=False, sigma=None, n_chains=1000,
                          observations=False, probs=.1, n_particles=1000, n_population=4820, mu=20, *,
                          rngs=None, keys=None, chains=1, seed=0, device=0, mh_ratio="reference",
-                         resample="multinomial", progress=False, filter_index_start=0, on_iteration=None):
-    """Run `chains` independent PMCMC chains (pmcmc.py:251-408 each) in lockstep.  `n_chains` keeps the
-    reference's meaning: MH iterations per chain.  Default rngs: np.random.RandomState(seed + c); default
-    keys: chain_key(seed, c).  Returns a list of ChainResult."""
+                         resample="multinomial", progress=False, filter_index_start=0, on_iteration=None,
+                         prefetch=0):
+    """Run `chains` independent PMCMC chains (pmcmc.py:251-408 each).  `n_chains` keeps the reference's
+    meaning: MH iterations per chain.  Default rngs: np.random.RandomState(seed + c); default keys:
+    chain_key(seed, c).  prefetch=0: lockstep, one batched filter per MH iteration (ChainSampler);
+    prefetch=K: speculative MH with max(K, chains) filter slots per batch (epipf.prefetch.PrefetchSampler,
+    same results).  Returns a list of ChainResult."""
     if rngs is None:
         rngs = [np.random.RandomState(seed + c) for c in range(chains)]
     if keys is None:
         keys = [chain_key(seed, c) for c in range(len(rngs))]
-    sampler = ChainSampler(Y, type_model, parameters, h, adaptive, sigma, n_chains, observations, probs, n_particles,
-                           n_population, mu, rngs=rngs, keys=keys, device=device, mh_ratio=mh_ratio,
-                           resample=resample, filter_index_start=filter_index_start)
+    args = (Y, type_model, parameters, h, adaptive, sigma, n_chains, observations, probs, n_particles, n_population, mu)
+    kw = dict(rngs=rngs, keys=keys, device=device, mh_ratio=mh_ratio, resample=resample,
+              filter_index_start=filter_index_start)
+    if prefetch:
+        from .prefetch import PrefetchSampler
+        sampler = PrefetchSampler(*args, slots=max(int(prefetch), len(rngs)), **kw)
+    else:
+        sampler = ChainSampler(*args, **kw)
     return sampler.run(progress=progress, on_iteration=on_iteration)
 
 
 def particle_mcmc(Y, type_model, parameters, h, adaptive=False, sigma=None, n_chains=1000, observations=False,
                   probs=.1, n_particles=1000, n_population=4820, mu=20, jobs=4, *, key=None, device=0,
-                  mh_ratio="reference", resample="multinomial", progress=True):
+                  mh_ratio="reference", resample="multinomial", progress=True, prefetch=32):
     """pmcmc.py:251-408 with the same signature and return value (thetas, likelihoods, sampled_trajs).
 
     Uses numpy's GLOBAL RandomState for proposals / acceptance / path picks, as the reference, and the
     module Philox stream (seed_stream) for the filters.  mh_ratio="reference" evaluates the reference's
     acceptance expression verbatim (linear likelihoods, MVN factors); "log" uses log-likelihoods and
-    stays correct when the likelihood underflows (T ≳ 150 observations)."""
+    stays correct when the likelihood underflows (T ≳ 150 observations).  prefetch=K evaluates up to K
+    speculative MH iterations per batched GPU launch (epipf.prefetch; identical results, and the global
+    RandomState ends where the sequential loop leaves it); prefetch=0 runs one filter per iteration."""
     k = _STREAM.key if key is None else key
     res = particle_mcmc_chains(Y, type_model, parameters, h, adaptive, sigma, n_chains, observations, probs,
                                n_particles, n_population, mu, rngs=[np.random], keys=[k], device=device,
                                mh_ratio=mh_ratio, resample=resample, progress=progress,
-                               filter_index_start=_STREAM.next_filter)[0]
+                               filter_index_start=_STREAM.next_filter, prefetch=prefetch)[0]
     if key is None:
         _STREAM.next_filter += res.filters_run
     return res.thetas, res.likelihoods, res.sampled_trajs.astype(np.float64)

@@ -1,0 +1,293 @@
+"""Prefetching (speculative) Metropolis-Hastings: one PMCMC chain advanced several iterations per GPU batch.
+
+The reference's MH loop (pmcmc.py:325-406) runs one particle filter per iteration, and iteration i+1's
+proposal depends on whether iteration i accepted, so a single chain is a sequential chain of filters.  One
+filter of N = 10^4 particles fills ~160 of the GPU's 1024 SIMDs; a single chain therefore runs at a small
+fraction of what the chip can do.  Prefetching MCMC (Brockwell 2006; Strid 2010) evaluates the filters of
+several FUTURE iterations at once, one per node of the tree of accept/reject outcomes:
+
+  * every random number the MH loop draws on the host (the proposal noise of multivariate_normal, the path
+    sampler's randint, the acceptance uniform) is replayed on a clone of the chain's RandomState, so each
+    speculative node carries exactly the proposal, pick and uniform the sequential run would draw if it took
+    that path.  The proposal of a node is noise + mean with the noise independent of the mean (numpy's
+    legacy multivariate_normal computes x = z @ (sqrt(s) v) then x += mean), so the accept and reject
+    children of a node share one draw;
+  * every filter is a pure function of (theta, probs, Philox key, filter index), and a node's
+    filter index is the count of filters on its path, so a speculative filter returns exactly what the
+    sequential run's filter would;
+  * each round schedules the K most probable unevaluated nodes (best first: accept branch weighted by the
+    chain's observed acceptance rate), runs their filters as ONE batched launch sequence (epipf_run over K
+    chain slots) plus on-device path sampling, then walks the realised path from the root as far as results
+    reach.  Nodes off the realised path are discarded; evaluated nodes below the new root are kept.
+
+The committed thetas, likelihoods, trajectories, acceptance count, filter count and the final RandomState
+state are identical to `ChainSampler`'s sequential run (tests/test_prefetch.py, tests/test_gpu_parity.py).
+"""
+import heapq
+import itertools
+
+import numpy as np
+
+from . import _lib
+from .pmcmc import ChainSampler, _log_ratio, _reference_ratio
+
+
+class _Val:
+    """A committed likelihood / trajectory (the root's current state)."""
+    __slots__ = ("z", "lz", "traj")
+
+    def __init__(self, z, lz, traj):
+        self.z, self.lz, self.traj = z, lz, traj
+
+
+class _Draws:
+    """Host draws of one MH iteration from one RandomState state (pmcmc.py:330 proposal, :241 path pick,
+    :395 acceptance uniform), replayed on a clone."""
+    __slots__ = ("delta", "s1", "chosen", "u", "s3")
+
+
+class _Node:
+    """State before MH iteration `i` on one path of one chain's outcome tree."""
+    __slots__ = ("chain", "i", "parent", "theta", "src", "state", "fnext", "box", "draws", "prop", "neg",
+                 "stripped", "theta_new", "result", "kids", "deg")
+
+    def __init__(self, chain, i, parent, theta, src, state, fnext, box=None):
+        self.chain, self.i, self.parent = chain, i, parent
+        self.theta = theta          # theta_{i-1}: the proposal mean
+        self.src = src              # _Val, or the filter node whose result is this state's likelihood
+        self.state = state          # RandomState state before iteration i
+        self.fnext = fnext          # filter index of the next filter on this path
+        self.box = box              # draws shared with the sibling (same state and proposal covariance)
+        self.draws = None
+        self.prop = None
+        self.neg = False
+        self.stripped = None
+        self.theta_new = None
+        self.result = None          # (log_zetas [T], status, trajectory [T, C]) once the filter ran
+        self.kids = None            # (accept, reject) or (negative,)
+        self.deg = None
+
+
+def _value(src):
+    """(z, lz, traj) of a node's current state, or None while its filter has not run."""
+    if isinstance(src, _Val):
+        return src.z, src.lz, src.traj
+    if src.result is None:
+        return None
+    lz = src.result[0]
+    return np.exp(lz[-1]), lz[-1], src.result[2]
+
+
+class PrefetchSampler(ChainSampler):
+    """`ChainSampler` (same arguments, same results) that evaluates up to `slots` speculative MH iterations per
+    batched filter launch, shared best-first among its chains."""
+
+    def __init__(self, *args, slots=32, **kw):
+        self.slots = max(1, int(slots))
+        kw["engine_chains"] = max(self.slots, int(kw.get("engine_chains", 0)))
+        super().__init__(*args, **kw)
+        self._std0 = [s.copy() for s in self.std]
+        self._scratch = np.random.RandomState(0)
+        self.roots = None
+        self._tick = itertools.count()
+        self.rounds = 0
+        self.speculative_filters = 0
+        self.degenerate = 0                                     # realised filters that returned (None, None, None)
+
+    # ------------------------------------------------------------------ host draws
+    def _std_for(self, node):
+        """Proposal covariance factor at iteration node.i (pmcmc.py:326-328: adaptive after 1000 iterations)."""
+        if not (self.adaptive and node.i > 1e3):
+            return self._std0[node.chain]
+        path = []
+        n = node
+        while n is not self.roots[node.chain]:
+            path.append(n.theta)
+            n = n.parent
+        th = np.concatenate([self.thetas[node.chain, :n.i], np.array(path[::-1]).reshape(-1, self.d)], axis=0)
+        return np.cov(th[:node.i].T, ddof=0) + 1e-4 * np.eye(self.d)
+
+    def _draw(self, state, std):
+        rs = self._scratch
+        rs.set_state(state)
+        dr = _Draws()
+        dr.delta = rs.multivariate_normal(np.zeros(self.d), self.h * std)
+        dr.s1 = rs.get_state()
+        dr.chosen = rs.randint(0, self.N)
+        dr.u = rs.uniform()
+        dr.s3 = rs.get_state()
+        return dr
+
+    def _expand(self, x):
+        """Proposal of iteration x.i and x's children (accept / reject, or the negative-proposal pass)."""
+        if x.kids is not None:
+            return
+        std = self._std_for(x)
+        shared = x.box is not None and not (self.adaptive and x.i > 1e3)
+        if shared and x.box[0] is not None:
+            dr = x.box[0]
+        else:
+            dr = self._draw(x.state, std)
+            if shared:
+                x.box[0] = dr
+        x.draws = dr
+        prop = dr.delta + x.theta                               # == multivariate_normal(theta, h*std), pmcmc.py:330
+        x.prop = prop
+        if sum(prop < 0) > 0:                                   # pmcmc.py:333-337: no filter this iteration
+            x.neg = True
+            x.kids = (_Node(x.chain, x.i + 1, x, x.theta, x.src, dr.s1, x.fnext),)
+            return
+        th, p2 = self._split(prop)
+        x.stripped = (th, p2)
+        x.theta_new = np.append(th, p2) if self.probs is None else prop
+        box = [None]
+        x.kids = (_Node(x.chain, x.i + 1, x, x.theta_new, x, dr.s3, x.fnext + 1, box),
+                  _Node(x.chain, x.i + 1, x, x.theta, x.src, dr.s3, x.fnext + 1, box))
+
+    def _degenerate_child(self, x):
+        if x.deg is None:                                       # pmcmc.py:365-369: no pick, no uniform drawn
+            x.deg = _Node(x.chain, x.i + 1, x, x.theta, x.src, x.draws.s1, x.fnext + 1)
+        return x.deg
+
+    def _decision(self, x):
+        """Realised child of an evaluated node, or None while its current likelihood is unknown."""
+        lzr, status, _ = x.result
+        if status != _lib.STATUS_OK:
+            return self._degenerate_child(x)
+        cur = _value(x.src)
+        if cur is None:
+            return None
+        z_old, lz_old, _ = cur
+        z_new = np.exp(lzr[-1])
+        if self.mh_ratio == "reference":
+            prob = _reference_ratio(z_new, z_old, x.theta_new, x.theta, self.parameters, self.h * self._std_for(x))
+        else:
+            prob = _log_ratio(lzr[-1], lz_old)
+        return x.kids[0] if x.draws.u < prob else x.kids[1]
+
+    # ------------------------------------------------------------------ rounds
+    def _alpha(self, c):
+        return (self.acceptances[c] - 1 + 1.0) / (self.filters_run[c] + 2.0)
+
+    def _schedule(self):
+        heap = []
+        for c, r in enumerate(self.roots):
+            heapq.heappush(heap, (-1.0, next(self._tick), r))
+        out = []
+        while heap and len(out) < self.slots:
+            negp, _, x = heapq.heappop(heap)
+            p = -negp
+            if x.i >= self.iters:
+                continue
+            self._expand(x)
+            if x.neg:
+                heapq.heappush(heap, (-p, next(self._tick), x.kids[0]))
+                continue
+            if x.result is None:
+                out.append(x)
+                a = self._alpha(x.chain)
+                heapq.heappush(heap, (-p * a, next(self._tick), x.kids[0]))
+                heapq.heappush(heap, (-p * (1.0 - a), next(self._tick), x.kids[1]))
+                continue
+            y = self._decision(x)
+            if y is not None:
+                heapq.heappush(heap, (-p, next(self._tick), y))
+            else:
+                a = self._alpha(x.chain)
+                heapq.heappush(heap, (-p * a, next(self._tick), x.kids[0]))
+                heapq.heappush(heap, (-p * (1.0 - a), next(self._tick), x.kids[1]))
+        return out
+
+    def _evaluate(self, nodes):
+        n = len(nodes)
+        th_all = np.zeros((n, self.dth))
+        pr_all = np.zeros(n)
+        keys = np.zeros(n, dtype=np.uint64)
+        fidx = np.zeros(n, dtype=np.uint64)
+        for s, x in enumerate(nodes):
+            th_all[s], pr_all[s] = x.stripped
+            keys[s] = self.keys[x.chain]
+            fidx[s] = x.fnext
+        lz, st = self.eng.run(th_all, pr_all, keys, fidx, observations=self.observations, resample=self.resample)
+        chosen = np.array([x.draws.chosen for x in nodes], dtype=np.int32)
+        tr = self.eng.path_sample(chosen) if np.any(st == _lib.STATUS_OK) else None
+        for s, x in enumerate(nodes):
+            x.result = (lz[s].copy(), int(st[s]), None if tr is None else tr[s])
+        self.last_active = n
+        self.speculative_filters += n
+        self.rounds += 1
+
+    def _commit(self, c, x, y, filtered, accepted):
+        i = x.i
+        z, lz, traj = _value(y.src)
+        self.thetas[c, i] = y.theta
+        self.likelihoods[c, i] = z
+        self.loglik[c, i] = lz
+        self.trajs[c, :, i, :] = traj
+        if filtered:
+            self.filters_run[c] += 1
+        if accepted:
+            self.acceptances[c] += 1
+
+    def _resolve(self):
+        """Walk every chain's realised path as far as the evaluated filters reach; returns iterations committed."""
+        done = 0
+        for c in range(self.nc):
+            x = self.roots[c]
+            while x.i < self.iters:
+                self._expand(x)
+                if x.neg:
+                    y = x.kids[0]
+                    self._commit(c, x, y, False, False)
+                elif x.result is None:
+                    break
+                else:
+                    y = self._decision(x)
+                    ok = x.result[1] == _lib.STATUS_OK
+                    self.degenerate += 0 if ok else 1
+                    self._commit(c, x, y, True, ok and y is x.kids[0])
+                x = y
+                done += 1
+            x.parent = None                                      # drop the discarded tree
+            self.roots[c] = x
+        return done
+
+    def initialise(self):
+        super().initialise()
+        self.roots = []
+        for c in range(self.nc):
+            st = self.rngs[c].get_state()
+            val = _Val(self.likelihoods[c, 0], self.loglik[c, 0], self.trajs[c, :, 0, :].copy())
+            self.roots.append(_Node(c, 1, None, self.thetas[c, 0].copy(), val, st, self.fnext[c]))
+
+    def advance(self):
+        """One round: schedule, evaluate (one batched filter of up to `slots` nodes), resolve.  Returns
+        (iterations committed, filters of the realised path among them)."""
+        f0 = sum(self.filters_run)
+        nodes = self._schedule()
+        if nodes:
+            self._evaluate(nodes)
+        done = self._resolve()
+        self.i = min(r.i for r in self.roots)
+        if self.i >= self.iters:
+            self._finish()
+        return done, sum(self.filters_run) - f0
+
+    def _finish(self):
+        for c in range(self.nc):
+            self.rngs[c].set_state(self.roots[c].state)      # the RandomState continues as after a sequential run
+            self.fnext[c] = self.roots[c].fnext
+
+    def step(self):
+        raise NotImplementedError("PrefetchSampler advances by rounds: use advance() or run()")
+
+    def run(self, progress=False, on_iteration=None):
+        if self.roots is None:
+            self.initialise()
+        while self.i < self.iters:
+            before = self.i
+            self.advance()
+            if on_iteration is not None:
+                for k in range(before, self.i):
+                    on_iteration(k, None)
+        return self.results()

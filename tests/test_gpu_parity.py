@@ -229,8 +229,9 @@ def test_dropin_particle_filter_signature(filter_golden):
         (None, None, None)
 
 
+@pytest.mark.parametrize("prefetch", [0, 32])
 @pytest.mark.parametrize("name", ["sir_small", "sir_p", "sub", "sir_adaptive"])
-def test_pmcmc_matches_reference_golden(pmcmc_golden, name):
+def test_pmcmc_matches_reference_golden(pmcmc_golden, name, prefetch):
     """particle_mcmc under np.random.seed(s) + seed_stream(key): identical accept/reject trace, thetas,
     sampled trajectories; likelihoods within 1e-9 relative."""
     from epipf import particle_mcmc, seed_stream
@@ -245,11 +246,38 @@ def test_pmcmc_matches_reference_golden(pmcmc_golden, name):
     np.random.seed(int(rec["seed"]))
     th, lk, tr = particle_mcmc(rec["Y"], model.lower(), list(rec["params"]), float(rec["h"]),
                                adaptive=bool(rec["adaptive"]), sigma=sigma, n_chains=int(rec["iters"]),
-                               probs=probs, n_particles=int(rec["N"]), n_population=npop, mu=mu, progress=False)
+                               probs=probs, n_particles=int(rec["N"]), n_population=npop, mu=mu, progress=False,
+                               prefetch=prefetch)
     assert G >= 1
     np.testing.assert_array_equal(th, rec["thetas"])
     np.testing.assert_array_equal(tr, rec["trajs"])
     np.testing.assert_allclose(lk, rec["likelihoods"], rtol=1e-9)
+
+
+@pytest.mark.parametrize("slots", [5, 48])
+def test_prefetch_equals_lockstep_on_device(datasets_golden, slots):
+    """Speculative MH (epipf.prefetch) on the GPU: one config-2-shaped chain (N=2000, T=200) and a 3-chain run,
+    every committed value and the final RandomState equal to the one-filter-per-iteration loop."""
+    from epipf.pmcmc import ChainSampler, chain_key
+    from epipf.prefetch import PrefetchSampler
+    Y = datasets_golden["cfg2_binom"]
+    for chains, h in ((1, 1e-4), (3, 1e-3)):
+        kw = dict(iters=30, probs=0.1, n_particles=2000, n_population=10000.0, mu=20.0, mh_ratio="log")
+        out = []
+        for cls, extra in ((ChainSampler, {}), (PrefetchSampler, {"slots": slots})):
+            rngs = [np.random.RandomState(40 + c) for c in range(chains)]
+            s = cls(Y, "sir", [0.25, 0.1], h, **kw, rngs=rngs, keys=[chain_key(40, c) for c in range(chains)],
+                    **extra)
+            out.append((s.run(), [r.get_state() for r in rngs], s))
+        (ra, sa, _), (rb, sb, pre) = out
+        for x, y in zip(ra, rb):
+            np.testing.assert_array_equal(x.thetas, y.thetas)
+            np.testing.assert_array_equal(x.log_likelihoods, y.log_likelihoods)
+            np.testing.assert_array_equal(x.sampled_trajs, y.sampled_trajs)
+            assert (x.acceptances, x.filters_run) == (y.acceptances, y.filters_run)
+        for u, v in zip(sa, sb):
+            assert np.array_equal(u[1], v[1]) and u[2:] == v[2:]
+        assert pre.rounds < 29
 
 
 def test_multichain_equals_single_chain(datasets_golden):
