@@ -93,12 +93,12 @@ struct epipf_ctx {
     void* abc = nullptr;
     bool abc_order = true;   // length-ordered ABC lanes (EPIPF_ABC_ORDER=0 disables)
     bool fast_ssa = true;    // certified f32 event loop (EPIPF_SSA_FAST=0 disables; results are identical)
-    int n_streams = kMaxFilterStreams;   // chain groups on concurrent streams (EPIPF_STREAMS overrides, 1..4)
-    hipStream_t aux[kMaxFilterStreams] = {nullptr, nullptr, nullptr, nullptr};
-    hipEvent_t join[kMaxFilterStreams] = {nullptr, nullptr, nullptr, nullptr};
+    int n_streams = 4;   // chain groups on concurrent streams (EPIPF_STREAMS overrides, 1..kMaxFilterStreams)
+    hipStream_t aux[kMaxFilterStreams] = {};
+    hipEvent_t join[kMaxFilterStreams] = {};
     hipEvent_t fork = nullptr;
-    hipEvent_t gb[kMaxFilterStreams] = {nullptr, nullptr, nullptr, nullptr};   // per-group step spans (timing)
-    hipEvent_t ge[kMaxFilterStreams] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t gb[kMaxFilterStreams] = {};   // per-group step spans (timing)
+    hipEvent_t ge[kMaxFilterStreams] = {};
     int last_groups = 1;
 };
 

@@ -125,7 +125,7 @@ struct AbcGatherArgs {
 
 // Streams of one filter run: group g of the chains runs on s[g]; s[0] is the context stream, the others have
 // waited for its inputs.  join[g] (g > 0) is recorded at the end of group g, and s[0] waits for all of them.
-constexpr int kMaxFilterStreams = 4;
+constexpr int kMaxFilterStreams = 8;
 struct FilterStreams {
     int n;
     hipStream_t s[kMaxFilterStreams];

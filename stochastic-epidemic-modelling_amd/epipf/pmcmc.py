@@ -341,6 +341,14 @@ class ChainSampler:
                             self.filters_run[c]) for c in range(self.nc)]
 
 
+def prefetch_slots(n_particles):
+    """Default speculative slots for one chain: about two resident waves per SIMD of filters in flight
+    (2048 waves of 64 particles; a round's latency barely grows until then), within [8, 64].  Config 2
+    (N = 10^4, 157 waves per filter) -> 13; scripts/prefetch_sweep.py measured 16 best there."""
+    waves = -(-int(n_particles) // 64)
+    return int(min(64, max(8, 2048 // waves)))
+
+
 def particle_mcmc_chains(Y, type_model, parameters, h, adaptive=False, sigma=None, n_chains=1000,
                          observations=False, probs=.1, n_particles=1000, n_population=4820, mu=20, *,
                          rngs=None, keys=None, chains=1, seed=0, device=0, mh_ratio="reference",
@@ -368,7 +376,7 @@ def particle_mcmc_chains(Y, type_model, parameters, h, adaptive=False, sigma=Non
 
 def particle_mcmc(Y, type_model, parameters, h, adaptive=False, sigma=None, n_chains=1000, observations=False,
                   probs=.1, n_particles=1000, n_population=4820, mu=20, jobs=4, *, key=None, device=0,
-                  mh_ratio="reference", resample="multinomial", progress=True, prefetch=32):
+                  mh_ratio="reference", resample="multinomial", progress=True, prefetch="auto"):
     """pmcmc.py:251-408 with the same signature and return value (thetas, likelihoods, sampled_trajs).
 
     Uses numpy's GLOBAL RandomState for proposals / acceptance / path picks, as the reference, and the
@@ -376,8 +384,11 @@ def particle_mcmc(Y, type_model, parameters, h, adaptive=False, sigma=None, n_ch
     acceptance expression verbatim (linear likelihoods, MVN factors); "log" uses log-likelihoods and
     stays correct when the likelihood underflows (T ≳ 150 observations).  prefetch=K evaluates up to K
     speculative MH iterations per batched GPU launch (epipf.prefetch; identical results, and the global
-    RandomState ends where the sequential loop leaves it); prefetch=0 runs one filter per iteration."""
+    RandomState ends where the sequential loop leaves it); "auto" sizes K to the particle count
+    (prefetch_slots); prefetch=0 runs one filter per iteration."""
     k = _STREAM.key if key is None else key
+    if prefetch == "auto":
+        prefetch = prefetch_slots(n_particles)
     res = particle_mcmc_chains(Y, type_model, parameters, h, adaptive, sigma, n_chains, observations, probs,
                                n_particles, n_population, mu, rngs=[np.random], keys=[k], device=device,
                                mh_ratio=mh_ratio, resample=resample, progress=progress,
