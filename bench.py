@@ -169,11 +169,25 @@ def main():
     bytes_per_unit = 8 * n_comp + 40                                  # 8C+40 B per particle-step
     achieved = units_per_launch * bytes_per_unit / avg_launch_s / 1e9
     traffic = None
+    valu = None
     pmc_path = os.path.join(REPO, "profiles", "pmc_step_kernel.json")
     if os.path.exists(pmc_path):
         try:
-            per_unit = json.load(open(pmc_path)).get("hbm_bytes_per_particle_step")
+            pmc = json.load(open(pmc_path))
+            per_unit = pmc.get("hbm_bytes_per_particle_step")
             traffic = per_unit * units_per_launch if per_unit else None
+            # the bound that matters: vector-instruction issue.  SQ_INSTS_VALU per particle-step of
+            # the committed PMC pass (whole-chip sum) x the live rate, against 1024 SIMD-32 x 2.4 GHz / 2 cycles per
+            # wave64 VALU instruction (MI355X_MICROARCH.md); the loop's mix (half VOP3 / 64-bit multiplies at ~4
+            # cycles) caps the reachable fraction near 0.55 of that peak
+            ins = pmc.get("pmc_avg_per_launch", {}).get("SQ_INSTS_VALU")
+            units = pmc.get("particle_steps_per_launch")
+            if ins and units and meta["model"] == "sir":
+                per_ps = ins / units
+                peak = 1024 * 2.4e9 / 2
+                valu = {"achieved": per_ps * value, "peak": peak, "unit": "wave64 VALU instr/s",
+                        "frac": per_ps * value / peak, "instr_per_particle_step": per_ps,
+                        "cycles_per_instr_at_2.4GHz": 1024 * 2.4e9 / (per_ps * value)}
         except (OSError, ValueError):
             traffic = None
     events_per_s = cst["events"] / (cst["step_ms"] / 1e3) if cst["step_ms"] > 0 else None
@@ -244,7 +258,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "pf_step_kernel", "avg_launch_us": avg_launch_s * 1e6,
                          "bytes_per_particle_step": bytes_per_unit, "particle_steps_per_launch": units_per_launch,
-                         "concurrent_launches_per_step": streams, "step_wall_us": step_wall_s * 1e6},
+                         "concurrent_launches_per_step": streams, "step_wall_us": step_wall_s * 1e6,
+                         "valu_issue": valu},
             "events_per_s": events_per_s,
             "ssa_lane_utilisation": lane_use,
             "resample_fallbacks": st["resample_fallbacks"],
