@@ -52,15 +52,10 @@ int dalloc(T** p, size_t n) {
 }
 
 int default_wg(int N) {
-    const char* e = getenv("EPIPF_WG");
-    if (e) {
-        int v = atoi(e);
-        if (v == 64 || v == 256) return v;
-    }
-    // One wave per block keeps the in-block CDF short, but every block holds the 2B-double block-sum table in
-    // LDS: past ~16k particles (B > 256) that table caps occupancy (N = 5e4: 15 KB per 64-thread block, 2.5
-    // waves/SIMD), so large filters use 256-thread blocks (B = N/256).
-    return N > 16384 ? 256 : 64;
+    // One wave per block at every N: the block-sum prefix is segmented (scan_segments), so a block's LDS does
+    // not grow with N.
+    (void)N;
+    return 64;
 }
 }  // namespace
 
@@ -106,7 +101,8 @@ struct epipf_ctx {
 // reduction tree behind every prefix: in-block scan (6 shuffle levels + <=4 wave offsets + 1) = 11 <= 16,
 // block-sum scan 16 + 2 * ceil(B / WG) sequential chunk adds, +2 for the final adds.
 static double cert_k(int N, int B, int wg) {
-    const int per = (B + wg - 1) / wg;
+    const int S = prefix_segment(B), nseg = (B + S - 1) / S;
+    const int per = ((nseg + wg - 1) / wg) * S;          // sequential block-sum adds per lane (scan_segments)
     const int D = 34 + 2 * per;
     return (double)N + 2.0 * D + 8.0;
 }
@@ -325,6 +321,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     a.cert_k = cert_k(c->N, c->B, c->wg);
     a.Y = c->Y; a.lf = c->lf; a.logtab = c->logtab; a.cp = c->cp; a.hidden = c->hidden; a.ancestry = c->ancestry;
     a.wraw = c->wraw; a.wloc = c->wloc; a.bsum = c->bsum; a.log_zeta = c->log_zeta; a.status = c->status;
+    a.seg = prefix_segment(c->B); a.nseg = (c->B + a.seg - 1) / a.seg;
     a.counters = c->counters;
     for (int g = 0; g < kMaxG; ++g) { a.npop[g] = c->npop[g]; a.mu[g] = c->mu[g]; a.emu[g] = c->emu[g]; a.kmax[g] = c->kmax[g]; }
 

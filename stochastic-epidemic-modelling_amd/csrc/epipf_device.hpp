@@ -776,6 +776,47 @@ __device__ __forceinline__ int resample_search(double U, const double* bpex, con
     return a;
 }
 
+// The same search over a segmented block-sum prefix (scan_segments in epipf_kernels.hip): level 1 over the LDS
+// segment ends seg_end[k] (S blocks per segment), level 2 walks the <= S block sums of the segment from global
+// memory with the scan's own additions (so every value equals the scan's), level 3 the block's in-block prefix.
+// With S = 1 this is resample_search above, value for value (seg_start = bpex, seg_end = bpex + bsum).
+__device__ __forceinline__ int resample_search_seg(double U, const double* seg_start, const double* seg_end, int nseg,
+                                                   int S, const double* __restrict__ bsum_g, int B, double total,
+                                                   const double* __restrict__ wloc, int WGB, int N, double cert_k,
+                                                   bool& certified) {
+    int lo = 0, hi = nseg - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (seg_end[mid] / total > U) hi = mid; else lo = mid + 1;
+    }
+    const int k = lo;
+    int b = k * S;
+    double base = seg_start[k];                                         // prefix before block b
+    if (S > 1) {
+        const int ie = min(b + S, B);
+        double e = base;
+        for (int i = b; i < ie; ++i) {
+            const double en = e + bsum_g[i];
+            if (en / total > U || i == ie - 1) { b = i; base = e; break; }
+            e = en;
+        }
+    }
+    const double* L = wloc + (size_t)b * WGB;
+    int l = 0, h = WGB - 1;
+    while (l < h) {
+        const int m = (l + h) >> 1;
+        if ((base + L[m]) / total > U) h = m; else l = m + 1;
+    }
+    const int a = b * WGB + l;
+    const double va = (base + L[l]) / total;
+    // inclusive prefix through block b-1: the segment's running sum, or the previous segment's end
+    const double pb = (b == k * S) ? (k > 0 ? seg_end[k - 1] : 0.0) : base;
+    const double vp = (l > 0) ? (base + L[l - 1]) / total : (b > 0 ? pb / total : -1.0);
+    certified = (va - cert_halfwidth(a, va, cert_k) > U) &&
+                (a == 0 || vp + cert_halfwidth(a - 1, vp, cert_k) < U) && a < N;
+    return a;
+}
+
 __device__ __forceinline__ double readlane_f64(double x, int l) {
     const long long b = __double_as_longlong(x);
     const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);

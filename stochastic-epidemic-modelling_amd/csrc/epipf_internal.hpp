@@ -28,6 +28,7 @@ __device__ __forceinline__ unsigned long long* counter_slot(unsigned long long* 
 struct StepArgs {
     int N, T, B, wg, max_chains, resample_mode, count_events, lf_max;
     int chain0;                   // first chain of this launch (chain groups run on separate streams)
+    int seg, nseg;                // block-sum prefix: S blocks per segment, ceil(B / S) segments (<= kMaxSegments)
     size_t hist_stride, anc_stride, wstride, bstride;
     double cert_k;                // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp)
     const double* Y;
@@ -135,6 +136,8 @@ struct FilterStreams {
 };
 
 size_t step_lds_bytes(int B, int wg);
+int prefix_segment(int B);
+constexpr int kMaxSegments = 200;
 hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, const FilterStreams& fs);
 hipError_t launch_path_sample(const PathArgs& a, hipStream_t s);
 hipError_t launch_log_table(LogTab* tab, hipStream_t s);

@@ -45,6 +45,33 @@ __device__ __forceinline__ double scan_block_sums(const double* __restrict__ bsu
     return bpex[B - 1] + bsum[B - 1];
 }
 
+// Segmented prefix of the B block sums (64-thread block): lane l sums the blocks of segments [l*q, (l+1)*q)
+// sequentially, a wave scan gives each lane its offset, and the lane writes seg_start[k] / seg_end[k] (the running
+// sum before / after segment k's S blocks) to LDS.  With S = 1 this is scan_block_sums<64> exactly (seg_start =
+// bpex, seg_end = bpex + bsum).  LDS holds 2 * nseg <= 400 doubles whatever N is, so one-wave blocks keep 7 waves
+// per SIMD at every size (before, past ~16k particles the 2B-double table capped occupancy and 256-thread blocks
+// were needed, whose four waves retire together).
+__device__ __forceinline__ double scan_segments(const double* __restrict__ bsum_g, int B, int S, int nseg,
+                                                double* seg_start, double* seg_end) {
+    const int lane = threadIdx.x;
+    const int q = (nseg + 63) / 64;
+    const int k0 = min(lane * q, nseg), k1 = min(k0 + q, nseg);
+    const int b0 = min(k0 * S, B), b1 = min(k1 * S, B);
+    double s = 0.0;
+    for (int i = b0; i < b1; ++i) s = s + bsum_g[i];
+    const double inc = block_inclusive_scan<64>(s, nullptr);
+    const double up = __shfl_up(inc, 1, 64);
+    double e = (lane == 0) ? 0.0 : up;
+    for (int k = k0; k < k1; ++k) {
+        seg_start[k] = e;
+        const int ie = min((k + 1) * S, B);
+        for (int i = k * S; i < ie; ++i) e = e + bsum_g[i];
+        seg_end[k] = e;
+    }
+    __syncthreads();
+    return seg_end[nseg - 1];
+}
+
 template <int MODEL, int G, int OBS, int WG>
 __global__ __launch_bounds__(WG) void pf_init_kernel(StepArgs a) {
     using Sh = Shape<MODEL, G>;
@@ -93,10 +120,11 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
     using Sh = Shape<MODEL, G>;
     constexpr int C = Sh::C;
     extern __shared__ __attribute__((aligned(16))) double smem[];
+    static_assert(WG == 64, "one wave per block (scan_segments)");
     LogTab* tab = reinterpret_cast<LogTab*>(smem);       // 128 x 16 B log table (first: 16-B aligned)
     double* red = smem + 2 * kLogTabEntries;             // WG/64 (+pad)
-    double* bsum = red + 16;                             // B
-    double* bpex = bsum + a.B;                           // B + WG
+    double* seg_start = red + 16;                        // S = 1: bsum [B] then bpex [B + WG]; else nseg + nseg
+    double* seg_end = seg_start + a.nseg;
     const int chain = a.chain0 + (int)blockIdx.y;
     const int tid = threadIdx.x;
     const int j = blockIdx.x * WG + tid;
@@ -110,7 +138,9 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
     const size_t bcur = ((size_t)cur * a.max_chains + chain) * a.bstride;
 
     // (b) likelihood: zetas[p] = zetas[p-1] * mean(w)  (pmcmc.py:183), kept in log space
-    const double total = scan_block_sums<WG>(a.bsum + bprev, a.B, bpex, bsum, red);
+    // S = 1 (B <= kMaxSegments): the block sums and their exclusive prefix stay in LDS; else segment ends only
+    const double total = (a.seg == 1) ? scan_block_sums<WG>(a.bsum + bprev, a.B, seg_start + a.B, seg_start, red)
+                                      : scan_segments(a.bsum + bprev, a.B, a.seg, a.nseg, seg_start, seg_end);
     if (!(total > 0.0)) {  // all weights 0 or NaN: numpy raises ValueError -> (None, None, None), :187-192
         if (blockIdx.x == 0 && tid == 0) {
             a.status[chain] = 1;
@@ -136,7 +166,12 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
             const Block r = philox(0u, 0u, rtag, cp.f, cp.k0, cp.k1);
             U = ((double)j + u01(r.x, r.y)) / (double)a.N;
         }
-        anc = resample_search<WG>(U, bpex, bsum, a.B, total, a.wloc + wprev, a.N, a.cert_k, certified);
+        if (a.seg == 1)
+            anc = resample_search<WG>(U, seg_start + a.B, seg_start, a.B, total, a.wloc + wprev, a.N, a.cert_k,
+                                      certified);
+        else
+            anc = resample_search_seg(U, seg_start, seg_end, a.nseg, a.seg, a.bsum + bprev, a.B, total,
+                                      a.wloc + wprev, WG, a.N, a.cert_k, certified);
     }
     if (__any(!certified)) {   // wave-uniform: the whole wave resolves its uncertified draws exactly
         const int e = resample_exact_wave(!certified, U, a.wraw + wprev, a.N);
@@ -266,7 +301,20 @@ __global__ __launch_bounds__(WG) void resample_search_kernel(ResampleArgs a) {
 }
 
 // ------------------------------------------------------------------------------- launchers
+// blocks per prefix segment: the smallest power of two with at most kMaxSegments segments
+int prefix_segment(int B) {
+    int S = 1;
+    while ((B + S - 1) / S > kMaxSegments) S <<= 1;
+    return S;
+}
+
 size_t step_lds_bytes(int B, int wg) {
+    const int S = prefix_segment(B);
+    if (S == 1) return sizeof(LogTab) * kLogTabEntries + sizeof(double) * (size_t)(16 + B + B + wg);
+    return sizeof(LogTab) * kLogTabEntries + sizeof(double) * (size_t)(16 + 2 * ((B + S - 1) / S));
+}
+
+static size_t resample_lds_bytes(int B, int wg) {
     return sizeof(LogTab) * kLogTabEntries + sizeof(double) * (size_t)(16 + B + B + wg);
 }
 
@@ -328,8 +376,8 @@ static hipError_t launch_model(const StepArgs& a, int model, int G, int obs, int
 }
 
 hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, const FilterStreams& fs) {
-    if (a.wg == 64) return launch_model<64>(a, model, G, obs, n_chains, fs);
-    return launch_model<256>(a, model, G, obs, n_chains, fs);
+    if (a.wg != 64) return hipErrorInvalidValue;
+    return launch_model<64>(a, model, G, obs, n_chains, fs);
 }
 
 hipError_t launch_log_table(LogTab* tab, hipStream_t s) {
@@ -365,7 +413,7 @@ hipError_t launch_simulate(const SimArgs& a, int model, int G, hipStream_t s) {
 
 hipError_t launch_resample(const ResampleArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(resample_scan_kernel<256>, dim3(a.B), dim3(256), sizeof(double) * 16, s, a);
-    hipLaunchKernelGGL(resample_search_kernel<256>, dim3(a.B), dim3(256), step_lds_bytes(a.B, 256), s, a);
+    hipLaunchKernelGGL(resample_search_kernel<256>, dim3(a.B), dim3(256), resample_lds_bytes(a.B, 256), s, a);
     return hipGetLastError();
 }
 

@@ -89,6 +89,25 @@ def test_filter_random_configs_vs_oracle(datasets_golden, seed):
     np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
 
 
+@pytest.mark.parametrize("N,chains", [(12800, 1), (12865, 2), (50000, 2), (140000, 1)])
+def test_filter_segmented_block_prefix_vs_oracle(datasets_golden, N, chains):
+    """N past 200 blocks of 64: the block-sum prefix is segmented (S = 2, 4, 16 blocks per segment; level 2 of the
+    resampling search walks a segment in global memory).  Bit-exact states/ancestors vs the oracle; every chain of a
+    batch, at the config-4 shape (pop 4820, ~500 events per particle-step)."""
+    Y = datasets_golden["sir_binom"][:4]
+    a = dict(Y=Y, model="sir", theta=(2.0, 1.0), N=N, npop=4820, mu=20)
+    eng, thv = engine_for(a, chains)
+    keys = [77 + c for c in range(chains)]
+    lz, st = eng.run(np.repeat(thv[None], chains, 0), [0.1] * chains, keys, [3] * chains)
+    hid, anc = eng.history(chains)
+    for c in range(chains):
+        o = oracle.particle_filter(Y, "sir", (2.0, 1.0), False, 0.1, N, 4820, 20, key=keys[c], filter_index=3)
+        assert int(st[c]) == o["status"] == 0
+        np.testing.assert_array_equal(hid[c], o["hidden"])
+        np.testing.assert_array_equal(anc[c], o["ancestry"])
+        np.testing.assert_allclose(lz[c], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
 def test_batched_chains_equal_single_runs(datasets_golden):
     """Chain c of a batched launch is bit-identical to running it alone (no cross-chain coupling),
     and inactive chains are skipped."""
