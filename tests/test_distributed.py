@@ -28,7 +28,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, Y, total, paths, q):
+def _worker(rank, world, port, Y, total, paths, q, prefetch=0):
     for p in paths:
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -40,7 +40,7 @@ def _worker(rank, world, port, Y, total, paths, q):
     pmw.get_engine = fge
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res, ids, th, ll = Dw.sharded_pmcmc(Y, "sir", [2.0, 1.0], 0.01, total, seed=9, **KW)
+        res, ids, th, ll = Dw.sharded_pmcmc(Y, "sir", [2.0, 1.0], 0.01, total, seed=9, prefetch=prefetch, **KW)
         q.put((rank, ids, th, ll))
     finally:
         dist.barrier()
@@ -71,8 +71,10 @@ def test_pack_unpack_roundtrip():
         np.testing.assert_array_equal(ll[c], res[c].log_likelihoods)
 
 
-@pytest.mark.parametrize("total", [3, 4])
-def test_gloo_world2_gather_equals_single_process(monkeypatch, datasets_golden, total):
+@pytest.mark.parametrize("total,prefetch", [(3, 0), (4, 0), (2, 4)])
+def test_gloo_world2_gather_equals_single_process(monkeypatch, datasets_golden, total, prefetch):
+    """prefetch > 0 with one chain per rank is the north star's one-chain-per-GPU layout, each chain speculative;
+    the gathered draws equal a one-process lockstep run of every chain."""
     Y = datasets_golden["cfg1_binom"][:6]
     monkeypatch.setattr(pm, "get_engine", fake_get_engine)
     _, ids, th1, ll1 = D.sharded_pmcmc(Y, "sir", [2.0, 1.0], 0.01, total, seed=9, **KW)
@@ -81,7 +83,7 @@ def test_gloo_world2_gather_equals_single_process(monkeypatch, datasets_golden, 
     q = ctx.Queue()
     port = _free_port()
     paths = [HERE] + [p for p in sys.path if "stochastic-epidemic" in p or p.endswith("oracle")]
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, Y, total, paths, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, Y, total, paths, q, prefetch)) for r in range(2)]
     for p in procs:
         p.start()
     out = {}
