@@ -342,11 +342,11 @@ class ChainSampler:
 
 
 def prefetch_slots(n_particles):
-    """Default speculative slots for one chain: about two resident waves per SIMD of filters in flight
-    (2048 waves of 64 particles; a round's latency barely grows until then), within [8, 64].  Config 2
-    (N = 10^4, 157 waves per filter) -> 13; scripts/prefetch_sweep.py measured 16 best there."""
+    """Default speculative slots for one chain: about 2.5 resident waves per SIMD of filters in flight
+    (2560 waves of 64 particles; a round's latency barely grows until then), within [8, 64].  Config 2
+    (N = 10^4, 157 waves per filter) -> 16, the best of scripts/prefetch_sweep.py's sweep there."""
     waves = -(-int(n_particles) // 64)
-    return int(min(64, max(8, 2048 // waves)))
+    return int(min(64, max(8, 2560 // waves)))
 
 
 def particle_mcmc_chains(Y, type_model, parameters, h, adaptive=False, sigma=None, n_chains=1000,

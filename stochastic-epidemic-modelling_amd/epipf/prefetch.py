@@ -6,12 +6,15 @@ filter of N = 10^4 particles fills ~160 of the GPU's 1024 SIMDs; a single chain 
 fraction of what the chip can do.  Prefetching MCMC (Brockwell 2006; Strid 2010) evaluates the filters of
 several FUTURE iterations at once, one per node of the tree of accept/reject outcomes:
 
-  * every random number the MH loop draws on the host (the proposal noise of multivariate_normal, the path
-    sampler's randint, the acceptance uniform) is replayed on a clone of the chain's RandomState, so each
-    speculative node carries exactly the proposal, pick and uniform the sequential run would draw if it took
-    that path.  The proposal of a node is noise + mean with the noise independent of the mean (numpy's
-    legacy multivariate_normal computes x = z @ (sqrt(s) v) then x += mean), so the accept and reject
-    children of a node share one draw;
+  * every random number the MH loop draws on the host (the proposal's standard normals, the path sampler's
+    randint, the acceptance uniform) comes from the chain's RandomState in a fixed per-iteration pattern that
+    does not depend on accept/reject: an iteration consumes d normals, then a pick and a uniform if its filter
+    ran and succeeded.  So every node at the same depth of the tree reads the same position of ONE replayed
+    stream (a clone of the RandomState drawn ahead once), and the proposal is numpy's legacy
+    multivariate_normal arithmetic on those normals: x = z @ (sqrt(s) v), x += mean (bit-identical, checked);
+    a negative proposal or a degenerate filter consumes the normals only, and its subtree forks a new stream
+    (rare: a replay from the stream's start).  The caller's RandomState advances along the realised path with
+    the same calls, so it ends exactly where the sequential loop leaves it;
   * every filter is a pure function of (theta, probs, Philox key, filter index), and a node's
     filter index is the count of filters on its path, so a speculative filter returns exactly what the
     sequential run's filter would;
@@ -40,25 +43,61 @@ class _Val:
         self.z, self.lz, self.traj = z, lz, traj
 
 
-class _Draws:
-    """Host draws of one MH iteration from one RandomState state (pmcmc.py:330 proposal, :241 path pick,
-    :395 acceptance uniform), replayed on a clone."""
-    __slots__ = ("delta", "s1", "chosen", "u", "s3")
+class _Stream:
+    """A clone of a chain's RandomState drawn ahead in the standard per-iteration pattern: position k holds the
+    proposal normals z (pmcmc.py:330), the path pick (:241) and the acceptance uniform (:395) of the k-th
+    iteration after the stream's start."""
+    SNAP = 32                       # a state snapshot every SNAP positions bounds a fork's replay
+
+    __slots__ = ("snaps", "rs", "z", "chosen", "u", "forks", "d", "N")
+
+    def __init__(self, state, d, N):
+        self.rs = np.random.RandomState()
+        self.rs.set_state(state)
+        self.snaps = {0: state}
+        self.z, self.chosen, self.u, self.forks = [], [], [], {}
+        self.d, self.N = d, N
+
+    def at(self, k):
+        while len(self.z) <= k:
+            n = len(self.z)
+            if n % self.SNAP == 0 and n not in self.snaps:
+                self.snaps[n] = self.rs.get_state()
+            self.z.append(self.rs.standard_normal(self.d))
+            self.chosen.append(self.rs.randint(0, self.N))
+            self.u.append(self.rs.uniform())
+        return self.z[k], self.chosen[k], self.u[k]
+
+    def fork(self, k):
+        """The stream after k standard iterations and the normals of one more (a negative proposal, or a filter
+        that returned (None, None, None): no pick and no uniform drawn)."""
+        f = self.forks.get(k)
+        if f is None:
+            self.at(k)
+            k0 = (k // self.SNAP) * self.SNAP
+            rs = np.random.RandomState()
+            rs.set_state(self.snaps[k0])
+            for _ in range(k - k0):
+                rs.standard_normal(self.d)
+                rs.randint(0, self.N)
+                rs.uniform()
+            rs.standard_normal(self.d)
+            f = self.forks[k] = _Stream(rs.get_state(), self.d, self.N)
+        return f
 
 
 class _Node:
     """State before MH iteration `i` on one path of one chain's outcome tree."""
-    __slots__ = ("chain", "i", "parent", "theta", "src", "state", "fnext", "box", "draws", "prop", "neg",
+    __slots__ = ("chain", "i", "parent", "theta", "src", "stream", "k", "fnext", "chosen", "u", "prop", "neg",
                  "stripped", "theta_new", "result", "kids", "deg")
 
-    def __init__(self, chain, i, parent, theta, src, state, fnext, box=None):
+    def __init__(self, chain, i, parent, theta, src, stream, k, fnext):
         self.chain, self.i, self.parent = chain, i, parent
         self.theta = theta          # theta_{i-1}: the proposal mean
         self.src = src              # _Val, or the filter node whose result is this state's likelihood
-        self.state = state          # RandomState state before iteration i
+        self.stream, self.k = stream, k   # host draws of iteration i: position k of the stream
         self.fnext = fnext          # filter index of the next filter on this path
-        self.box = box              # draws shared with the sibling (same state and proposal covariance)
-        self.draws = None
+        self.chosen = self.u = None
         self.prop = None
         self.neg = False
         self.stripped = None
@@ -87,7 +126,7 @@ class PrefetchSampler(ChainSampler):
         kw["engine_chains"] = max(self.slots, int(kw.get("engine_chains", 0)))
         super().__init__(*args, **kw)
         self._std0 = [s.copy() for s in self.std]
-        self._scratch = np.random.RandomState(0)
+        self._factor0 = [self._factor(s) for s in self._std0]
         self.roots = None
         self._tick = itertools.count()
         self.rounds = 0
@@ -95,6 +134,11 @@ class PrefetchSampler(ChainSampler):
         self.degenerate = 0                                     # realised filters that returned (None, None, None)
 
     # ------------------------------------------------------------------ host draws
+    def _factor(self, std):
+        """sqrt(s)[:, None] * vh of svd(h * std): numpy's legacy multivariate_normal transform."""
+        _, sv, vh = np.linalg.svd(self.h * std)
+        return np.sqrt(sv)[:, None] * vh
+
     def _std_for(self, node):
         """Proposal covariance factor at iteration node.i (pmcmc.py:326-328: adaptive after 1000 iterations)."""
         if not (self.adaptive and node.i > 1e3):
@@ -107,46 +151,32 @@ class PrefetchSampler(ChainSampler):
         th = np.concatenate([self.thetas[node.chain, :n.i], np.array(path[::-1]).reshape(-1, self.d)], axis=0)
         return np.cov(th[:node.i].T, ddof=0) + 1e-4 * np.eye(self.d)
 
-    def _draw(self, state, std):
-        rs = self._scratch
-        rs.set_state(state)
-        dr = _Draws()
-        dr.delta = rs.multivariate_normal(np.zeros(self.d), self.h * std)
-        dr.s1 = rs.get_state()
-        dr.chosen = rs.randint(0, self.N)
-        dr.u = rs.uniform()
-        dr.s3 = rs.get_state()
-        return dr
-
     def _expand(self, x):
         """Proposal of iteration x.i and x's children (accept / reject, or the negative-proposal pass)."""
         if x.kids is not None:
             return
-        std = self._std_for(x)
-        shared = x.box is not None and not (self.adaptive and x.i > 1e3)
-        if shared and x.box[0] is not None:
-            dr = x.box[0]
+        z, x.chosen, x.u = x.stream.at(x.k)
+        if self.adaptive and x.i > 1e3:
+            fac = self._factor(self._std_for(x))
         else:
-            dr = self._draw(x.state, std)
-            if shared:
-                x.box[0] = dr
-        x.draws = dr
-        prop = dr.delta + x.theta                               # == multivariate_normal(theta, h*std), pmcmc.py:330
+            fac = self._factor0[x.chain]
+        prop = np.dot(z.reshape(-1, self.d), fac)               # == multivariate_normal(theta, h*std), pmcmc.py:330
+        prop += x.theta
+        prop = prop.reshape(self.d)
         x.prop = prop
-        if sum(prop < 0) > 0:                                   # pmcmc.py:333-337: no filter this iteration
+        if (prop < 0).any():                                    # sum(prop < 0) > 0, pmcmc.py:333-337: no filter
             x.neg = True
-            x.kids = (_Node(x.chain, x.i + 1, x, x.theta, x.src, dr.s1, x.fnext),)
+            x.kids = (_Node(x.chain, x.i + 1, x, x.theta, x.src, x.stream.fork(x.k), 0, x.fnext),)
             return
         th, p2 = self._split(prop)
         x.stripped = (th, p2)
         x.theta_new = np.append(th, p2) if self.probs is None else prop
-        box = [None]
-        x.kids = (_Node(x.chain, x.i + 1, x, x.theta_new, x, dr.s3, x.fnext + 1, box),
-                  _Node(x.chain, x.i + 1, x, x.theta, x.src, dr.s3, x.fnext + 1, box))
+        x.kids = (_Node(x.chain, x.i + 1, x, x.theta_new, x, x.stream, x.k + 1, x.fnext + 1),
+                  _Node(x.chain, x.i + 1, x, x.theta, x.src, x.stream, x.k + 1, x.fnext + 1))
 
     def _degenerate_child(self, x):
         if x.deg is None:                                       # pmcmc.py:365-369: no pick, no uniform drawn
-            x.deg = _Node(x.chain, x.i + 1, x, x.theta, x.src, x.draws.s1, x.fnext + 1)
+            x.deg = _Node(x.chain, x.i + 1, x, x.theta, x.src, x.stream.fork(x.k), 0, x.fnext + 1)
         return x.deg
 
     def _decision(self, x):
@@ -163,7 +193,7 @@ class PrefetchSampler(ChainSampler):
             prob = _reference_ratio(z_new, z_old, x.theta_new, x.theta, self.parameters, self.h * self._std_for(x))
         else:
             prob = _log_ratio(lzr[-1], lz_old)
-        return x.kids[0] if x.draws.u < prob else x.kids[1]
+        return x.kids[0] if x.u < prob else x.kids[1]
 
     # ------------------------------------------------------------------ rounds
     def _alpha(self, c):
@@ -209,7 +239,7 @@ class PrefetchSampler(ChainSampler):
             keys[s] = self.keys[x.chain]
             fidx[s] = x.fnext
         lz, st = self.eng.run(th_all, pr_all, keys, fidx, observations=self.observations, resample=self.resample)
-        chosen = np.array([x.draws.chosen for x in nodes], dtype=np.int32)
+        chosen = np.array([x.chosen for x in nodes], dtype=np.int32)
         tr = self.eng.path_sample(chosen) if np.any(st == _lib.STATUS_OK) else None
         for s, x in enumerate(nodes):
             x.result = (lz[s].copy(), int(st[s]), None if tr is None else tr[s])
@@ -218,6 +248,12 @@ class PrefetchSampler(ChainSampler):
         self.rounds += 1
 
     def _commit(self, c, x, y, filtered, accepted):
+        """Iteration x.i realised as y.  The caller's RandomState draws what the sequential loop would."""
+        rng = self.rngs[c]
+        rng.standard_normal(self.d)                             # the proposal's normals (multivariate_normal)
+        if filtered and x.result[1] == _lib.STATUS_OK:
+            rng.randint(0, self.N)                              # path pick, pmcmc.py:241
+            rng.uniform()                                       # acceptance uniform, :395
         i = x.i
         z, lz, traj = _value(y.src)
         self.thetas[c, i] = y.theta
@@ -256,9 +292,9 @@ class PrefetchSampler(ChainSampler):
         super().initialise()
         self.roots = []
         for c in range(self.nc):
-            st = self.rngs[c].get_state()
+            stream = _Stream(self.rngs[c].get_state(), self.d, self.N)
             val = _Val(self.likelihoods[c, 0], self.loglik[c, 0], self.trajs[c, :, 0, :].copy())
-            self.roots.append(_Node(c, 1, None, self.thetas[c, 0].copy(), val, st, self.fnext[c]))
+            self.roots.append(_Node(c, 1, None, self.thetas[c, 0].copy(), val, stream, 0, self.fnext[c]))
 
     def advance(self):
         """One round: schedule, evaluate (one batched filter of up to `slots` nodes), resolve.  Returns
@@ -275,7 +311,6 @@ class PrefetchSampler(ChainSampler):
 
     def _finish(self):
         for c in range(self.nc):
-            self.rngs[c].set_state(self.roots[c].state)      # the RandomState continues as after a sequential run
             self.fnext[c] = self.roots[c].fnext
 
     def step(self):
