@@ -27,7 +27,7 @@ def test_mh_loop_reproduces_reference_trace(oracle_engine, pmcmc_golden, name):
                                   adaptive=bool(rec["adaptive"]), sigma=sigma, n_chains=int(rec["iters"]),
                                   probs=probs, n_particles=int(rec["N"]),
                                   n_population=rec["npop"] if sub else float(rec["npop"][0]),
-                                  mu=rec["mu"] if sub else float(rec["mu"][0]), progress=False)
+                                  mu=rec["mu"] if sub else float(rec["mu"][0]), progress=False, prefetch=0)
     np.testing.assert_array_equal(th, rec["thetas"])
     np.testing.assert_array_equal(tr, rec["trajs"])
     np.testing.assert_allclose(lk, rec["likelihoods"], rtol=1e-9)
