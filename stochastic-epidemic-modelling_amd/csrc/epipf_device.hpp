@@ -515,13 +515,19 @@ struct FastSubgroups {                                                 // gilles
         for (int q = 0; q < G; ++q) { Sd[q] = (double)S[q]; Id[q] = (double)I[q]; }
         return subgroups_channel_exact<G>(cp.theta, Sd, Id, sumN, u);
     }
+    // Channel ch = g*(G+1) + c: c < G is infection s_{g}_{c} (S[c] -> I[c], :183), c = G recovery i_{g} (I[g] -> R,
+    // :185).  Only one group moves, q = c or g: a per-group select instead of a branch per channel (the compiler
+    // turns the channel-by-channel form into a divergent switch).
     __device__ __forceinline__ void apply(int ch, float s) {
+        const int g = ch / (G + 1), c = ch - g * (G + 1);
+        const bool inf = c < G;
+        const int q = inf ? c : g;
+        const float dS = inf ? s : 0.f, dI = inf ? s : -s;
 #pragma unroll
-        for (int q = 0; q < G; ++q) {
-#pragma unroll
-            for (int q2 = 0; q2 < G; ++q2)
-                if (ch == q * (G + 1) + q2) { S[q2] -= s; I[q2] += s; }        // s_{g}_{g2}: :183
-            if (ch == q * (G + 1) + G) I[q] -= s;                             // i_{g}: :185
+        for (int r = 0; r < G; ++r) {
+            const bool hit = q == r;
+            S[r] -= hit ? dS : 0.f;
+            I[r] += hit ? dI : 0.f;
         }
     }
     __device__ __forceinline__ int save(double* x) const {
