@@ -39,8 +39,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--single-chain", action="store_true",
-                    help="also time 1 chain/GPU: one filter per MH iteration, and speculative MH (extra fields)")
+    ap.add_argument("--single-chain", action=argparse.BooleanOptionalAction, default=True,
+                    help="also time 1 chain/GPU (N=1 only): one filter per MH iteration, and speculative MH (extra fields)")
     ap.add_argument("--prefetch", type=int, default=16, help="filter slots per round of the speculative single chain")
     ap.add_argument("--prefetch-iters", type=int, default=60, help="MH iterations timed for the speculative chain")
     return ap.parse_args()

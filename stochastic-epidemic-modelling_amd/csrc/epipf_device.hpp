@@ -609,21 +609,13 @@ __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, 
     return true;
 }
 
-// One particle over [0, tmax] (every lane of the wave starts together, so the event index k is wave-uniform).
-// Software pipelining: event k+1's Philox block (counter-based, so independent of event k's outcome) is
-// computed while event k's f64 work runs, which gives each wave two independent dependency chains.  The
-// block drawn after the last event is discarded (one per particle-step).  Lanes first try the certified f32
-// path; lanes it cannot certify run this exact loop from the untouched parent state.
+// The exact loop over [0, tmax] from the parent state x (every lane that enters starts at event 0 together, so
+// the event index k is wave-uniform).  Software pipelining: event k+1's Philox block (counter-based, so
+// independent of event k's outcome) is computed while event k's f64 work runs, which gives each wave two
+// independent dependency chains.  The block drawn after the last event is discarded (one per particle-step).
 template <int MODEL, int G>
-__device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
-                                             double tmax, const LogTab* __restrict__ tab, int& iters, int& exact) {
-    int fast_iters = 0, fast_nev = 0;
-    exact = 1;
-    if (fast_propagate<MODEL, G>(x, cp, j, ptag, tmax, fast_nev, fast_iters)) {
-        iters = fast_iters;
-        exact = 0;
-        return fast_nev;
-    }
+__device__ __forceinline__ int exact_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
+                                               double tmax, const LogTab* __restrict__ tab, int& iters) {
     SsaState<MODEL, G> st;
     st.load(x, cp);
     double t = 0.0;
@@ -641,7 +633,25 @@ __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, ui
         alive = ev && st.active();
     }
     st.save(x);
-    iters = (int)k + fast_iters;
+    iters = (int)k;
+    return nev;
+}
+
+// One particle over [0, tmax]: the certified f32 path first; lanes it cannot certify run the exact loop from the
+// untouched parent state.
+template <int MODEL, int G>
+__device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
+                                             double tmax, const LogTab* __restrict__ tab, int& iters, int& exact) {
+    int fast_iters = 0, fast_nev = 0;
+    exact = 1;
+    if (fast_propagate<MODEL, G>(x, cp, j, ptag, tmax, fast_nev, fast_iters)) {
+        iters = fast_iters;
+        exact = 0;
+        return fast_nev;
+    }
+    int ex_iters = 0;
+    const int nev = exact_propagate<MODEL, G>(x, cp, j, ptag, tmax, tab, ex_iters);
+    iters = ex_iters + fast_iters;
     return nev;
 }
 

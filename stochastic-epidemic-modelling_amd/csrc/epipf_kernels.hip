@@ -16,6 +16,10 @@
 
 #include "epipf_internal.hpp"
 
+#ifndef EPIPF_STEP_WAVES
+#define EPIPF_STEP_WAVES 1   // minimum waves per SIMD asked of the step kernel's register allocation
+#endif
+
 namespace epipf {
 
 // exclusive prefix of the B block sums into LDS (bpex), deterministic order; returns the total.
@@ -116,7 +120,7 @@ __global__ __launch_bounds__(WG) void pf_init_kernel(StepArgs a) {
 }
 
 template <int MODEL, int G, int OBS, int WG>
-__global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
+__global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs a, int p) {
     using Sh = Shape<MODEL, G>;
     constexpr int C = Sh::C;
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -129,7 +133,6 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
     const int tid = threadIdx.x;
     const int j = blockIdx.x * WG + tid;
     if (a.status[chain] != 0) return;
-    for (int i = tid; i < kLogTabEntries; i += WG) tab[i] = a.logtab[i];    // published by the barriers below
     const ChainParam cp = a.cp[chain];
     const int prev = (p - 1) & 1, cur = p & 1;
     const size_t wprev = ((size_t)prev * a.max_chains + chain) * a.wstride;
@@ -180,16 +183,33 @@ __global__ __launch_bounds__(WG) void pf_step_kernel(StepArgs a, int p) {
             atomicAdd(counter_slot(a.counters) + 1, 1ull);
         }
     }
+    // (f) gather the parent state, (g) propagate over [0, 1], :195-220: the certified f32 loop, then the exact loop
+    // for the lanes it hands back.  The exact loop's log table is copied to LDS only by waves that need it (~1.5%
+    // at config 2): one wave per block, so the wave-uniform test is block-uniform and the barrier is legal.
+    double x[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = 0.0;
+    const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
+    bool fast_ok = false;
     if (j < a.N) {
         anc = min(max(anc, 0), a.N - 1);
         a.ancestry[(size_t)chain * a.anc_stride + (size_t)p * a.N + j] = anc;   // :193
-        // (f) gather the parent state, (g) propagate over [0, 1], :195-220
         const int32_t* hp = a.hidden + (size_t)chain * a.hist_stride + ((size_t)(p - 1) * a.N + anc) * C;
-        double x[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) x[c] = (double)hp[c];
-        const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
-        nev = ssa_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, tab, iters, exact);
+        fast_ok = fast_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, nev, iters);
+    }
+    exact = (j < a.N && !fast_ok) ? 1 : 0;
+    if (__any(exact != 0)) {
+        for (int i = tid; i < kLogTabEntries; i += WG) tab[i] = a.logtab[i];
+        __syncthreads();
+        if (exact) {
+            int ex_iters = 0;
+            nev = exact_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, tab, ex_iters);
+            iters += ex_iters;
+        }
+    }
+    if (j < a.N) {
         int32_t* hc = a.hidden + (size_t)chain * a.hist_stride + ((size_t)p * a.N + j) * C;
 #pragma unroll
         for (int c = 0; c < C; ++c) hc[c] = (int32_t)x[c];                        // :222-231
