@@ -19,6 +19,6 @@ if [[ $what == all || $what == smoke ]]; then step smoke 300 python -c "import _
 if [[ $what == all || $what == tests ]]; then step pytest_gpu 900 python -m pytest tests -m gpu -q -rf; fi
 if [[ $what == all || $what == bench ]]; then step bench 600 python bench.py --steps 5 --warmup 1 --single-chain; fi
 if [[ $what == all || $what == prof ]]; then
-    step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
+    step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-single-chain
 fi
 echo "== done"

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r1}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BENCH="bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
+BENCH="bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-single-chain ${BENCH_ARGS:-}"
 step() {  # step <name> <timeout> <cmd...>
     local name=$1 t=$2; shift 2
     echo "== $name ($(date +%T))"

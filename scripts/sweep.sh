@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 out=gpurun_out/sweep.jsonl; : > $out
 for ch in ${CHAINS:-1 8 16 32 48 64 128 256}; do
   echo "== chains=$ch"
-  timeout -k 10 300 python bench.py --chains $ch --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline > gpurun_out/sweep_one.log 2>&1
+  timeout -k 10 300 python bench.py --chains $ch --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-single-chain > gpurun_out/sweep_one.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "rc=$rc"; tail -5 gpurun_out/sweep_one.log; exit $rc; fi
   tail -1 gpurun_out/sweep_one.log >> $out
