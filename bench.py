@@ -32,7 +32,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--chains", type=int, default=int(os.environ.get("EPIPF_BENCH_CHAINS", 128)),
+    ap.add_argument("--chains", type=int, default=int(os.environ.get("EPIPF_BENCH_CHAINS", 256)),
                     help="independent MH chains per GPU (batched in one launch per filter step)")
     ap.add_argument("--particles", type=int, default=None, help="default: the config's N (SURVEY.md §8d)")
     ap.add_argument("--config", type=int, default=2)
@@ -170,6 +170,7 @@ def main():
     achieved = units_per_launch * bytes_per_unit / avg_launch_s / 1e9
     traffic = None
     valu = None
+    rocprof_us = None
     pmc_path = os.path.join(REPO, "profiles", "pmc_step_kernel.json")
     if os.path.exists(pmc_path):
         try:
@@ -180,6 +181,7 @@ def main():
             # the committed PMC pass (whole-chip sum) x the live rate, against 1024 SIMD-32 x 2.4 GHz / 2 cycles per
             # wave64 VALU instruction (MI355X_MICROARCH.md); the loop's mix (half VOP3 / 64-bit multiplies at ~4
             # cycles) caps the reachable fraction near 0.55 of that peak
+            rocprof_us = pmc.get("trace_avg_us")
             ins = pmc.get("pmc_avg_per_launch", {}).get("SQ_INSTS_VALU")
             units = pmc.get("particle_steps_per_launch")
             if ins and units and meta["model"] == "sir":
@@ -259,6 +261,10 @@ def main():
                          "kernel": "pf_step_kernel", "avg_launch_us": avg_launch_s * 1e6,
                          "bytes_per_particle_step": bytes_per_unit, "particle_steps_per_launch": units_per_launch,
                          "concurrent_launches_per_step": streams, "step_wall_us": step_wall_s * 1e6,
+                         # the same kernel's average dispatch duration in the committed rocprofv3 trace of this
+                         # command (profiles/pmc_step_kernel.json); the HIP-event figure above also counts the time a
+                         # launch waits for CUs held by the concurrent chain-group launches
+                         "rocprof_avg_launch_us": rocprof_us,
                          "valu_issue": valu},
             "events_per_s": events_per_s,
             "ssa_lane_utilisation": lane_use,
