@@ -766,14 +766,19 @@ __device__ __forceinline__ double cert_halfwidth(int i, double v, double cert_k)
 // Two-level search of v (bpex: exclusive prefix of the block sums and bsum: block sums, both in LDS;
 // wloc: in-block inclusive prefix, in HBM/L2).  Returns the candidate index; `certified` says whether the
 // bracket test above proved it.
+// The search itself compares prefixes against U * total (one multiply instead of an IEEE division per level);
+// only the final bracket is evaluated on v = prefix / total.  Where the two orders disagree (a prefix within an
+// ulp of U * total) the candidate is off by one, its bracket test fails and the exact fallback decides, so the
+// result is still numpy's.
 template <int WG>
 __device__ __forceinline__ int resample_search(double U, const double* bpex, const double* bsum, int B,
                                                double total, const double* wloc, int N, double cert_k,
                                                bool& certified) {
+    const double Ut = U * total;
     int lo = 0, hi = B - 1;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if ((bpex[mid] + bsum[mid]) / total > U) hi = mid; else lo = mid + 1;
+        if (bpex[mid] + bsum[mid] > Ut) hi = mid; else lo = mid + 1;
     }
     const int b = lo;
     const double base = bpex[b];
@@ -781,7 +786,7 @@ __device__ __forceinline__ int resample_search(double U, const double* bpex, con
     int l = 0, h = WG - 1;
     while (l < h) {
         const int m = (l + h) >> 1;
-        if ((base + L[m]) / total > U) h = m; else l = m + 1;
+        if (base + L[m] > Ut) h = m; else l = m + 1;
     }
     const int a = b * WG + l;
     const double va = (base + L[l]) / total;
@@ -800,10 +805,11 @@ __device__ __forceinline__ int resample_search_seg(double U, const double* seg_s
                                                    int S, const double* __restrict__ bsum_g, int B, double total,
                                                    const double* __restrict__ wloc, int WGB, int N, double cert_k,
                                                    bool& certified) {
+    const double Ut = U * total;                                        // search on U * total (resample_search)
     int lo = 0, hi = nseg - 1;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (seg_end[mid] / total > U) hi = mid; else lo = mid + 1;
+        if (seg_end[mid] > Ut) hi = mid; else lo = mid + 1;
     }
     const int k = lo;
     int b = k * S;
@@ -813,7 +819,7 @@ __device__ __forceinline__ int resample_search_seg(double U, const double* seg_s
         double e = base;
         for (int i = b; i < ie; ++i) {
             const double en = e + bsum_g[i];
-            if (en / total > U || i == ie - 1) { b = i; base = e; break; }
+            if (en > Ut || i == ie - 1) { b = i; base = e; break; }
             e = en;
         }
     }
@@ -821,7 +827,7 @@ __device__ __forceinline__ int resample_search_seg(double U, const double* seg_s
     int l = 0, h = WGB - 1;
     while (l < h) {
         const int m = (l + h) >> 1;
-        if ((base + L[m]) / total > U) h = m; else l = m + 1;
+        if (base + L[m] > Ut) h = m; else l = m + 1;
     }
     const int a = b * WGB + l;
     const double va = (base + L[l]) / total;
