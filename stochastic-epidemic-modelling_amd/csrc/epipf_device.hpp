@@ -368,13 +368,13 @@ template <int G> struct SsaState<kSubgroups2, G> : SubgroupsState<G> {};
 //   clock    time is kept in units of 1/ln 2 and counted down: rem = tmax/ln2 + sum(log2(x_f) * rcp(total)),
 //            the event is inside the step iff rem >= 0 (the exact path's t + tau <= tmax, scaled).  x_f = 1 - U
 //            from two converts (relative error <= 3 ulp for x >= 2^-20); v_log_f32 is within 2 ulp of |log2 x|
-//            on every float in [2^-20, 1) (exhaustive, scripts/f32_accuracy.hip).  Per event
+//            on every float in [2^-20, 1) (exhaustive, scripts/f32_accuracy.hip); below 2^-20 (2^-20 of events)
+//            log2 is taken in f64 of the exact x and rounded (tiny_log2, <= 0.5 ulp + 2^-29).  Per event
 //            |tau2_f - tau2| <= (e_as + 5.5) ulp |tau2_f| + 4.4 ulp rcp(total), so with R = sum rcp(total) the
 //            remaining time is within B = kClockT tmax/ln2 + 5 ulp R of the exact path's, scaled
 //            (kClockT = e_as + 7 ulp covers the float evaluation of B and rem and at most 2^26 events).
 //            rem > B: the event is the exact path's; rem < -B: the step ends there, as in the exact path;
-//            otherwise (and for x < 2^-20, probability 2^-20 per event) the lane hands its whole step to the
-//            exact loop, from the untouched parent state.
+//            otherwise the lane hands its whole step to the exact loop, from the untouched parent state.
 // Eligible lanes: population < 2^24 (counts exact in f32; < 2^26 events per step) and every rate parameter
 // zero or in [2^-60, 2^40] (every f32 intermediate stays normal).
 constexpr float kUlpF = 0x1.0p-24f;
@@ -382,6 +382,11 @@ constexpr float kClockRF = 5.0f * kUlpF;
 constexpr double kInvLn2 = 0x1.71547652b82fep0;
 
 __device__ __forceinline__ bool rate_ok(float v) { return v == 0.f || (v >= 0x1.0p-60f && v <= 0x1.0p40f); }
+
+// log2(1 - U) for 1 - U < 2^-20, where the two-convert f32 form of 1 - U loses its relative accuracy: the exact
+// 53-bit 1 - U in f64 and the library log2 (<= 1 ulp f64), rounded to f32 (<= 0.5 ulp + 2^-29), inside the 2-ulp
+// log budget of the clock bound.  Out of line: it runs for 2^-20 of events.
+__device__ __noinline__ float tiny_log2(uint32_t lo, uint32_t hi) { return (float)log2(one_minus_u01(lo, hi)); }
 
 template <int MODEL, int G>
 struct FastSsa;
@@ -559,7 +564,7 @@ __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, 
     const float Bt = (float)rem * F::kClockT;
     float R = 0.f, df = 0.f, B = 0.f;
     uint32_t ks = 0;                                                   // event index, wave-uniform (SGPR)
-    bool alive = st.active(), ok = true, tiny = false;
+    bool alive = st.active(), ok = true;
     int ch = 0;
     Block rn{0u, 0u, 0u, 0u};
     if (alive) rn = philox<true>(0u, j, ptag, cp.f, cp.k0, cp.k1);    // x word inverted: ~x
@@ -590,18 +595,19 @@ __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, 
         }
         if (close) ch = st.exact_channel(cp, u01(r.z, r.w));
         const uint32_t nh = ~r.y;
-        const float xf = fmaf((float)nh, 0x1.0p-32f, (float)r.x * 0x1.0p-64f);     // 1 - U (r.x is ~x)
-        rem = rem + (double)(__builtin_amdgcn_logf(xf) * ri);          // np.random.exponential
+        float lg;
+        if (nh < 4096u) lg = tiny_log2(~r.x, r.y);                    // 1 - U < 2^-20: 2^-20 of events
+        else lg = __builtin_amdgcn_logf(fmaf((float)nh, 0x1.0p-32f, (float)r.x * 0x1.0p-64f));  // 1 - U (r.x is ~x)
+        rem = rem + (double)(lg * ri);                                 // np.random.exponential
         R += ri;
         df = (float)rem;
         B = fmaf(R, kClockRF, Bt);
-        tiny = nh < 4096u;
-        ok = df > B && !tiny;                                          // certainly inside the step
+        ok = df > B;                                                   // certainly inside the step
         st.apply(ch, 1.f);                                             // undone below if the lane overshoots
         alive = ok && st.active();
     }
     if (!ok) {
-        if (tiny || !(df < -B)) return false;                         // boundary too close to call: exact loop
+        if (!(df < -B)) return false;                                 // boundary too close to call: exact loop
         st.apply(ch, -1.f);                                            // the overshooting event is not applied
     }
     nev_out = st.save(x);
