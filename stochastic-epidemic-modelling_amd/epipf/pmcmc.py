@@ -142,6 +142,21 @@ def _reference_ratio(z_new, z_old, theta_new, theta_old, parameters, cov):
     return min(1, prob)
 
 
+def mvn_factor(cov):
+    """numpy's legacy RandomState.multivariate_normal(mean, cov) draws z = standard_normal(d) and returns
+    z @ (sqrt(s)[:, None] * vh) + mean with (u, s, vh) = svd(cov).  The factor depends on cov only, so a cached
+    factor gives bit-identical proposals with the same RNG consumption, without an SVD per draw (67 us -> 3 us)."""
+    _, sv, vh = np.linalg.svd(np.asarray(cov, dtype=np.float64))
+    return np.sqrt(sv)[:, None] * vh
+
+
+def mvn_apply(z, fac, mean):
+    """The rest of the legacy multivariate_normal arithmetic: np.dot(z, fac), then += mean."""
+    x = np.dot(z.reshape(-1, fac.shape[0]), fac)
+    x += mean
+    return x.reshape(fac.shape[0])
+
+
 def _log_ratio(lz_new, lz_old):
     """Underflow-free MH acceptance probability min(1, z'/z) from log-likelihoods (the symmetric
     Gaussian proposal terms of pmcmc.py:380-391 cancel)."""
@@ -201,12 +216,19 @@ class ChainSampler:
         self.loglik = np.zeros((nc, self.iters))
         self.trajs = np.zeros((nc, T, self.iters, Cc))
         self.std = [np.eye(d) if sigma is None else np.asarray(sigma, dtype=np.float64) for _ in range(nc)]
+        self._fac = [None] * nc                                  # multivariate_normal factor of h * std[c]
         self.fnext = [int(filter_index_start)] * nc
         self.filters_run = [0] * nc
         self.acceptances = [1] * nc
         self.dth = d - (1 if probs is None else 0)
         self.i = 0
         self.last_active = 0
+
+    def _propose(self, c, mean):
+        """rngs[c].multivariate_normal(mean, h * std[c]) (pmcmc.py:277, :330) with the SVD factor cached per chain."""
+        if self._fac[c] is None:
+            self._fac[c] = mvn_factor(self.h * self.std[c])
+        return mvn_apply(self.rngs[c].standard_normal(self.d), self._fac[c], mean)
 
     def _split(self, prop):
         """probs / subgroup reshaping, pmcmc.py:283-296 and :339-352 (the subgroup beta matrix is the
@@ -256,7 +278,7 @@ class ChainSampler:
         while pending:
             props = {}
             for c in pending:
-                prop = self.rngs[c].multivariate_normal(np.array(self.parameters), self.h * self.std[c])
+                prop = self._propose(c, np.array(self.parameters))
                 if sum(prop < 0) > 0:
                     continue
                 props[c] = prop
@@ -278,41 +300,52 @@ class ChainSampler:
         self.i = 1
 
     def step(self):
-        """One MH iteration for every chain, pmcmc.py:325-406.  Returns the number of chains that ran a filter."""
+        """One MH iteration for every chain, pmcmc.py:325-406.  Returns the number of chains that ran a filter.
+        Per chain the RNG calls keep the reference's order (proposal normals, path-pick randint, acceptance
+        uniform); the bookkeeping (accepted rows, copies of the previous row) is one array assignment per field."""
         i = self.i
         props = {}
         for c in range(self.nc):
             if self.adaptive and i > 1e3:
                 self.std[c] = np.cov(self.thetas[c, :i].T, ddof=0) + 1e-4 * np.eye(self.d)
-            prop = self.rngs[c].multivariate_normal(self.thetas[c, i - 1], self.h * self.std[c])
-            if sum(prop < 0) > 0:
-                self._copy_prev(c, i)
+                self._fac[c] = None
+            prop = self._propose(c, self.thetas[c, i - 1])
+            if (prop < 0).any():                                  # sum(prop < 0) > 0, pmcmc.py:333-337
                 continue
             props[c] = prop
+        acc = []
         if props:
             lz, st, stripped = self._run_batch(props)
-            ok = [c for c in props if st[c] == _lib.STATUS_OK]
+            ok = [c for c in props if st[c] == _lib.STATUS_OK]     # degenerate filters: rejected, :365-369
             tr = self._path_sample(ok) if ok else None
-            for c in props:
-                if st[c] != _lib.STATUS_OK:
-                    self._copy_prev(c, i)
-                    continue
+            new_th = []
+            for c in ok:
                 th, p2 = stripped[c]
                 theta_new = np.append(th, p2) if self.probs is None else props[c]
-                z_new = np.exp(lz[c, -1])
                 if self.mh_ratio == "reference":
-                    prob = _reference_ratio(z_new, self.likelihoods[c, i - 1], theta_new, self.thetas[c, i - 1],
-                                            self.parameters, self.h * self.std[c])
+                    prob = _reference_ratio(np.exp(lz[c, -1]), self.likelihoods[c, i - 1], theta_new,
+                                            self.thetas[c, i - 1], self.parameters, self.h * self.std[c])
                 else:
                     prob = _log_ratio(lz[c, -1], self.loglik[c, i - 1])
                 if self.rngs[c].uniform() < prob:
+                    acc.append(c)
+                    new_th.append(theta_new)
+            if acc:
+                a = np.asarray(acc)
+                self.thetas[a, i] = np.asarray(new_th)
+                self.loglik[a, i] = lz[a, -1]
+                self.likelihoods[a, i] = np.exp(lz[a, -1])
+                self.trajs[a, :, i, :] = tr[a]
+                for c in acc:
                     self.acceptances[c] += 1
-                    self.thetas[c, i] = theta_new
-                    self.likelihoods[c, i] = z_new
-                    self.loglik[c, i] = lz[c, -1]
-                    self.trajs[c, :, i, :] = tr[c]
-                else:
-                    self._copy_prev(c, i)
+        rej = np.ones(self.nc, dtype=bool)
+        rej[acc] = False
+        if rej.any():                                             # rejected, negative or degenerate: previous row
+            r = np.flatnonzero(rej)
+            self.thetas[r, i] = self.thetas[r, i - 1]
+            self.likelihoods[r, i] = self.likelihoods[r, i - 1]
+            self.loglik[r, i] = self.loglik[r, i - 1]
+            self.trajs[r, :, i, :] = self.trajs[r, :, i - 1, :]
         self.i += 1
         return len(props)
 

@@ -32,7 +32,7 @@ import itertools
 import numpy as np
 
 from . import _lib
-from .pmcmc import ChainSampler, _log_ratio, _reference_ratio
+from .pmcmc import ChainSampler, _log_ratio, _reference_ratio, mvn_apply, mvn_factor
 
 
 class _Val:
@@ -136,8 +136,7 @@ class PrefetchSampler(ChainSampler):
     # ------------------------------------------------------------------ host draws
     def _factor(self, std):
         """sqrt(s)[:, None] * vh of svd(h * std): numpy's legacy multivariate_normal transform."""
-        _, sv, vh = np.linalg.svd(self.h * std)
-        return np.sqrt(sv)[:, None] * vh
+        return mvn_factor(self.h * std)
 
     def _std_for(self, node):
         """Proposal covariance factor at iteration node.i (pmcmc.py:326-328: adaptive after 1000 iterations)."""
@@ -160,9 +159,7 @@ class PrefetchSampler(ChainSampler):
             fac = self._factor(self._std_for(x))
         else:
             fac = self._factor0[x.chain]
-        prop = np.dot(z.reshape(-1, self.d), fac)               # == multivariate_normal(theta, h*std), pmcmc.py:330
-        prop += x.theta
-        prop = prop.reshape(self.d)
+        prop = mvn_apply(z, fac, x.theta)                       # == multivariate_normal(theta, h*std), pmcmc.py:330
         x.prop = prop
         if (prop < 0).any():                                    # sum(prop < 0) > 0, pmcmc.py:333-337: no filter
             x.neg = True

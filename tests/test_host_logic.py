@@ -62,3 +62,28 @@ def test_multichain_lockstep_equals_independent_runs(oracle_engine, datasets_gol
         np.testing.assert_array_equal(single.thetas, multi[c].thetas)
         np.testing.assert_array_equal(single.sampled_trajs, multi[c].sampled_trajs)
         np.testing.assert_allclose(single.log_likelihoods, multi[c].log_likelihoods)
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 5])
+def test_cached_mvn_factor_equals_legacy_multivariate_normal(d):
+    """ChainSampler draws proposals as mvn_apply(standard_normal(d), mvn_factor(cov), mean) with the factor cached
+    per chain: the same values, bit for bit, and the same RandomState consumption as numpy's legacy
+    multivariate_normal(mean, cov) (pmcmc.py:277, :330), for isotropic, correlated and adaptive-style covariances."""
+    rs = np.random.RandomState(11 + d)
+    for trial in range(600):
+        h = 10.0 ** rs.uniform(-6, 0)
+        if trial % 3 == 0:
+            cov = h * np.eye(d)
+        else:
+            a = rs.standard_normal((d + 3, d))
+            cov = h * (np.cov(a.T, ddof=0).reshape(d, d) + 1e-4 * np.eye(d))
+        mean = rs.uniform(0, 3, d)
+        seed = int(rs.randint(0, 2**31))
+        ref, mine = np.random.RandomState(seed), np.random.RandomState(seed)
+        fac = pm.mvn_factor(cov)
+        for _ in range(3):
+            a_ = ref.multivariate_normal(mean, cov)
+            b_ = pm.mvn_apply(mine.standard_normal(d), fac, mean)
+            assert a_.shape == b_.shape == (d,)
+            assert np.array_equal(a_, b_), (cov, a_, b_)
+        assert ref.uniform() == mine.uniform()          # same stream position afterwards
