@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--single-chain", action=argparse.BooleanOptionalAction, default=True,
                     help="also time 1 chain/GPU (N=1 only): one filter per MH iteration, and speculative MH (extra fields)")
+    ap.add_argument("--pipelines", type=int, default=int(os.environ.get("EPIPF_BENCH_PIPELINES", 1)),
+                    help="chain groups on their own engine + host thread, so each group's MH host work overlaps the "
+                         "others' filters (epipf.pmcmc.run_pipelined); 1 = one lockstep sampler")
     ap.add_argument("--prefetch", type=int, default=16, help="filter slots per round of the speculative single chain")
     ap.add_argument("--prefetch-iters", type=int, default=60, help="MH iterations timed for the speculative chain")
     return ap.parse_args()
@@ -102,46 +105,70 @@ def main():
 
     from epipf import datasets
     from epipf.distributed import gather_draws, pack_draws, shard
-    from epipf.pmcmc import ChainSampler, chain_key
+    from epipf.engine import Engine
+    from epipf.pmcmc import ChainSampler, chain_key, run_pipelined
 
     Y, meta = datasets.benchmark_dataset(args.config)
     N, T = (args.particles or meta["N"]), Y.shape[0]
     C = args.chains
     gid = shard(C * world, world, rank)                              # global chain ids of this rank
-    sampler = ChainSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=args.warmup + args.steps + 2,
-                           observations=meta.get("observations", False), probs=meta["probs"], n_particles=N,
-                           n_population=meta["n_population"], mu=meta["mu"],
-                           rngs=[np.random.RandomState(args.seed + g) for g in gid],
-                           keys=[chain_key(args.seed, g) for g in gid], device=local, mh_ratio="log")
-    eng = sampler.eng
-    sampler.initialise()
-    for _ in range(args.warmup):
-        sampler.step()
+    P = max(1, min(args.pipelines, C))
+    streams_env = max(1, min(int(os.environ.get("EPIPF_STREAMS", 4)), 8))
+    samplers = []
+    for k in range(P):                                               # contiguous chain groups, one engine each
+        ids = gid[k * C // P:(k + 1) * C // P]
+        kw = {}
+        if P > 1:
+            eng_k = Engine(meta["model"], len(np.atleast_1d(meta["n_population"])), N, T, len(ids), device=local)
+            eng_k.set_streams(max(1, streams_env // P))
+            kw["engine"] = eng_k
+        samplers.append(ChainSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=args.warmup + args.steps + 2,
+                                     observations=meta.get("observations", False), probs=meta["probs"], n_particles=N,
+                                     n_population=meta["n_population"], mu=meta["mu"],
+                                     rngs=[np.random.RandomState(args.seed + g) for g in ids],
+                                     keys=[chain_key(args.seed, g) for g in ids], device=local, mh_ratio="log", **kw))
+    engines = [s.eng for s in samplers]
+    streams = P * max(1, streams_env // P) if P > 1 else min(streams_env, C)   # concurrent step launches
+    for s_ in samplers:
+        s_.initialise()
+    run_pipelined(samplers, args.warmup) if P > 1 else [samplers[0].step() for _ in range(args.warmup)]
 
     def barrier():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
 
+    def stats_sum():
+        tot = {}
+        for e in engines:
+            for k, v in e.stats().items():
+                tot[k] = tot.get(k, 0) + v
+        return tot
+
     from epipf import _lib
-    eng.reset_stats()
-    eng.set_profiling(_lib.PROFILE_TIMING)       # HIP events only: the timed kernels are the production ones
+    for e in engines:
+        e.reset_stats()
+        e.set_profiling(_lib.PROFILE_TIMING)     # HIP events only: the timed kernels are the production ones
     barrier()
     t0 = time.perf_counter()
-    filters = 0
-    for _ in range(args.steps):
-        filters += sampler.step()
+    if P > 1:
+        filters = run_pipelined(samplers, args.steps)
+    else:
+        filters = sum(samplers[0].step() for _ in range(args.steps))
     # end of run: gather every rank's posterior draws over RCCL (xGMI), SURVEY.md §8e
-    gathered = gather_draws(pack_draws(sampler.results(), upto=sampler.i), local)
+    results = [r for s_ in samplers for r in s_.results()]
+    gathered = gather_draws(pack_draws(results, upto=samplers[0].i), local)
     barrier()
     dt = time.perf_counter() - t0
-    st = eng.stats()
+    st = stats_sum()
     # one extra, untimed MH iteration with device counters on: SSA events/s and SIMD lane use
-    eng.reset_stats()
-    eng.set_profiling(_lib.PROFILE_COUNTERS)
-    sampler.step()
-    eng.set_profiling(_lib.PROFILE_OFF)
-    cst = eng.stats()
+    for e in engines:
+        e.reset_stats()
+        e.set_profiling(_lib.PROFILE_COUNTERS)
+    run_pipelined(samplers, 1) if P > 1 else samplers[0].step()
+    for e in engines:
+        e.set_profiling(_lib.PROFILE_OFF)
+    cst = stats_sum()
 
     # max over ranks of the wall time; sum of filters
     if dist is not None:
@@ -160,7 +187,6 @@ def main():
     # per chain group on its own stream.  The roofline is per kernel launch, as rocprofv3 sees it:
     # HIP events on each group's stream span its back-to-back step kernels (launch-to-completion, so a kernel
     # waiting for CUs held by the other groups counts; rocprofv3's durations do not); the step wall time too.
-    streams = max(1, min(int(os.environ.get("EPIPF_STREAMS", 4)), C))
     launches = max(1, st["step_kernel_launches"])
     avg_launch_s = st["step_kernel_ms"] / 1e3 / launches
     step_wall_s = st["step_ms"] / 1e3 / max(1, st["step_launches"])
@@ -192,7 +218,8 @@ def main():
                         "cycles_per_instr_at_2.4GHz": 1024 * 2.4e9 / (per_ps * value)}
         except (OSError, ValueError):
             traffic = None
-    events_per_s = cst["events"] / (cst["step_ms"] / 1e3) if cst["step_ms"] > 0 else None
+    # SSA events per second of job time: events per particle-step (counters iteration) x the measured rate
+    events_per_s = value * cst["events"] / cst["particle_steps"] if cst["particle_steps"] else None
     lane_use = cst["lane_iterations"] / cst["wave_lane_slots"] if cst["wave_lane_slots"] else None
 
     single = prefetch = None
@@ -255,6 +282,7 @@ def main():
             "config": {"workload": f"BASELINE config {args.config}: {meta['model'].upper()} PMCMC, N={N} particles, "
                                    f"pop={meta['n_population']}, {T} obs, {C} independent chains per GPU",
                        "particles": N, "T_obs": T, "chains_per_gpu": C, "population": meta["n_population"],
+                       "pipelines": P,
                        "parallelism": f"chains sharded over {world} GPU(s), RCCL all-gather of draws at end"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

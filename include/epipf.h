@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define EPIPF_ABI_VERSION 2
+#define EPIPF_ABI_VERSION 3
 
 /* return codes */
 #define EPIPF_OK 0
@@ -158,6 +158,12 @@ int epipf_abc_trials(epipf_ctx* ctx, const double* Y, int T, const double* prior
 #define EPIPF_PROFILE_TIMING 1
 #define EPIPF_PROFILE_COUNTERS 2
 int epipf_set_profiling(epipf_ctx* ctx, int level);
+
+/* Chain groups of one epipf_run on concurrent HIP streams (1..8, default 4 or EPIPF_STREAMS): each group's T-1
+   step kernels run back to back on its own stream so that one group's launch tail overlaps the others' work.
+   Engine tuning only, no reference counterpart; results do not depend on it.  A host that runs several contexts
+   from separate threads (MH iterations pipelined with the device, epipf.pmcmc.run_pipelined) sets 1 each. */
+int epipf_set_streams(epipf_ctx* ctx, int n_streams);
 int epipf_get_stats(epipf_ctx* ctx, epipf_stats* out);
 int epipf_reset_stats(epipf_ctx* ctx);
 

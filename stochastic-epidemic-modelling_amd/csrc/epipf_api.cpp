@@ -135,6 +135,18 @@ static void free_ctx(epipf_ctx* c) {
     delete c;
 }
 
+// Streams and events of chain groups 0..n-1 (group 0 runs on c->stream), created on first use.
+static bool ensure_streams(epipf_ctx* c, int n) {
+    for (int g = 0; g < n; ++g) {
+        if (!c->gb[g] && hipEventCreate(&c->gb[g]) != hipSuccess) return false;
+        if (!c->ge[g] && hipEventCreate(&c->ge[g]) != hipSuccess) return false;
+        if (g == 0) continue;
+        if (!c->aux[g] && hipStreamCreateWithFlags(&c->aux[g], hipStreamNonBlocking) != hipSuccess) return false;
+        if (!c->join[g] && hipEventCreateWithFlags(&c->join[g], hipEventDisableTiming) != hipSuccess) return false;
+    }
+    return true;
+}
+
 extern "C" {
 
 const char* epipf_last_error(void) { return g_err.c_str(); }
@@ -208,17 +220,6 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
         free_ctx(c);
         return fail(EPIPF_EHIP, "hipEventCreate failed");
     }
-    for (int g = 0; g < c->n_streams; ++g)
-        if (hipEventCreate(&c->gb[g]) != hipSuccess || hipEventCreate(&c->ge[g]) != hipSuccess) {
-            free_ctx(c);
-            return fail(EPIPF_EHIP, "hipEventCreate failed");
-        }
-    for (int g = 1; g < c->n_streams; ++g)
-        if (hipStreamCreateWithFlags(&c->aux[g], hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&c->join[g], hipEventDisableTiming) != hipSuccess) {
-            free_ctx(c);
-            return fail(EPIPF_EHIP, "auxiliary stream creation failed");
-        }
     if (launch_log_table(c->logtab, c->stream) != hipSuccess ||
         hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
@@ -327,6 +328,9 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
 
     FilterStreams fs{};
     fs.n = std::min(c->n_streams, n_chains);
+    // Created on first use, not with the context: HIP maps streams onto its few hardware queues in creation order,
+    // so contexts that each run one group (run_pipelined) get one stream each and land on different queues.
+    if (!ensure_streams(c, fs.n)) return fail(EPIPF_EHIP, "auxiliary stream creation failed");
     fs.s[0] = c->stream;
     if (fs.n > 1) HIP_TRY(hipEventRecord(c->fork, c->stream));    // the groups' inputs are on c->stream
     for (int g = 1; g < fs.n; ++g) {
@@ -753,6 +757,14 @@ int epipf_set_profiling(epipf_ctx* c, int enable) {
     if (!c) return fail(EPIPF_EINVAL, "NULL context");
     if (enable < EPIPF_PROFILE_OFF || enable > EPIPF_PROFILE_COUNTERS) return fail(EPIPF_EINVAL, "bad profiling level %d", enable);
     c->profiling = enable;
+    return EPIPF_OK;
+}
+
+int epipf_set_streams(epipf_ctx* c, int n_streams) {
+    if (!c) return fail(EPIPF_EINVAL, "NULL context");
+    if (n_streams < 1 || n_streams > kMaxFilterStreams)
+        return fail(EPIPF_EINVAL, "n_streams %d outside [1, %d]", n_streams, kMaxFilterStreams);
+    c->n_streams = n_streams;     // streams are created at the first run that uses them
     return EPIPF_OK;
 }
 

@@ -198,6 +198,10 @@ class Engine:
             level = _lib.PROFILE_OFF
         check(self._L.epipf_set_profiling(self._h, int(level)), "epipf_set_profiling")
 
+    def set_streams(self, n):
+        """Concurrent chain-group streams used by run() (1..8)."""
+        check(self._L.epipf_set_streams(self._h, int(n)), "epipf_set_streams")
+
     def stats(self):
         s = _lib.Stats()
         check(self._L.epipf_get_stats(self._h, ctypes.byref(s)), "epipf_get_stats")

@@ -188,7 +188,7 @@ class ChainSampler:
 
     def __init__(self, Y, type_model, parameters, h, adaptive=False, sigma=None, iters=1000, observations=False,
                  probs=.1, n_particles=1000, n_population=4820, mu=20, *, rngs, keys, device=0,
-                 mh_ratio="reference", resample="multinomial", filter_index_start=0, engine_chains=0):
+                 mh_ratio="reference", resample="multinomial", filter_index_start=0, engine_chains=0, engine=None):
         self.rngs = list(rngs)
         self.keys = np.asarray(keys, dtype=np.uint64)
         nc = self.nc = len(self.rngs)
@@ -208,7 +208,13 @@ class ChainSampler:
         Cc = n_compartments(mid, G)
         npop, mus = _population(mid, G, n_population, mu)
         self.iters = int(iters)
-        eng = self.eng = get_engine(mid, G, n_particles, T, max(nc, int(engine_chains)), device)
+        if engine is None:
+            eng = get_engine(mid, G, n_particles, T, max(nc, int(engine_chains)), device)
+        else:                                                     # a private context (run_pipelined)
+            eng = engine
+            if (eng.model, eng.G, eng.N) != (mid, G, self.N) or eng.t_max < T or eng.max_chains < max(nc, engine_chains):
+                raise ValueError("engine does not match the model / particles / T / chains of this sampler")
+        self.eng = eng
         eng.set_observations(Y)
         eng.set_population(npop, mus)
         self.thetas = np.zeros((nc, self.iters, d))
@@ -372,6 +378,36 @@ class ChainSampler:
     def results(self):
         return [ChainResult(self.thetas[c], self.likelihoods[c], self.loglik[c], self.trajs[c], self.acceptances[c],
                             self.filters_run[c]) for c in range(self.nc)]
+
+
+def run_pipelined(samplers, steps):
+    """Advance independent ChainSamplers `steps` MH iterations each, one host thread per sampler, and return the
+    number of filters run.  Each sampler must own its engine (ChainSampler(..., engine=Engine(...))): a filter call
+    releases the GIL for its whole device run (ctypes), so one sampler's host work (proposals, path picks,
+    accept/reject) overlaps the other samplers' filters on the device instead of leaving it idle between MH
+    iterations.  Every sampler's chains, draws and results are exactly those of calling its step() `steps` times."""
+    import threading
+    engines = [id(s.eng) for s in samplers]
+    if len(set(engines)) != len(engines):
+        raise ValueError("run_pipelined needs one engine per sampler")
+    counts = [0] * len(samplers)
+    errors = []
+
+    def work(k):
+        try:
+            for _ in range(steps):
+                counts[k] += samplers[k].step()
+        except BaseException as e:  # noqa: BLE001 -- re-raised in the caller's thread
+            errors.append(e)
+
+    threads = [threading.Thread(target=work, args=(k,), daemon=True) for k in range(len(samplers))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0]
+    return sum(counts)
 
 
 def prefetch_slots(n_particles):

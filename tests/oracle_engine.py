@@ -13,6 +13,7 @@ class OracleEngine:
 
     def __init__(self, mid, G, N, T, chains):
         self.mid, self.G, self.N, self.t_max, self.max_chains = mid, G, N, T, chains
+        self.model = mid
         self.C = n_compartments(mid, G)
         self.hist = {}
 

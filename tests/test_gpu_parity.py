@@ -312,6 +312,51 @@ def test_multichain_equals_single_chain(datasets_golden):
         np.testing.assert_array_equal(single.sampled_trajs, multi[c].sampled_trajs)
 
 
+def test_stream_groups_and_pipelines_do_not_change_results(datasets_golden):
+    """epipf_set_streams (1, 3, 8 chain groups) leaves every chain bit-identical, and run_pipelined over private
+    engines (bench.py --pipelines) equals one lockstep sampler over the same chains."""
+    from epipf.engine import Engine
+    from epipf.pmcmc import ChainSampler, chain_key, run_pipelined
+    Y = datasets_golden["cfg2_binom"][:60]
+    eng = Engine("sir", 1, 3000, Y.shape[0], 9)
+    eng.set_observations(Y)
+    eng.set_population(10000, 20)
+    th = np.tile([0.25, 0.1], (9, 1)) + np.linspace(0, 0.02, 9)[:, None]
+    ref = None
+    for n in (1, 3, 8):
+        eng.set_streams(n)
+        lz, st = eng.run(th, 0.1, np.arange(9) + 50, 2)
+        hid, anc = eng.history(9)
+        if ref is None:
+            ref = (lz, st, hid, anc)
+            continue
+        for x, y in zip(ref, (lz, st, hid, anc)):
+            np.testing.assert_array_equal(x, y)
+    with pytest.raises(Exception):
+        eng.set_streams(9)
+    eng.close()
+    kw = dict(iters=8, probs=0.1, n_particles=2000, n_population=10000.0, mu=20.0, mh_ratio="log")
+    whole = ChainSampler(Y, "sir", [0.25, 0.1], 1e-3, **kw, rngs=[np.random.RandomState(60 + g) for g in range(6)],
+                         keys=[chain_key(60, g) for g in range(6)])
+    whole.initialise()
+    ran = sum(whole.step() for _ in range(7))
+    parts = []
+    for grp in ([0, 1, 2], [3], [4, 5]):
+        e = Engine("sir", 1, 2000, Y.shape[0], len(grp))
+        e.set_streams(1)
+        parts.append(ChainSampler(Y, "sir", [0.25, 0.1], 1e-3, **kw, rngs=[np.random.RandomState(60 + g) for g in grp],
+                                  keys=[chain_key(60, g) for g in grp], engine=e))
+    for s in parts:
+        s.initialise()
+    assert run_pipelined(parts, 7) == ran
+    for a, b in zip(whole.results(), [r for s in parts for r in s.results()]):
+        np.testing.assert_array_equal(a.thetas, b.thetas)
+        np.testing.assert_array_equal(a.log_likelihoods, b.log_likelihoods)
+        np.testing.assert_array_equal(a.sampled_trajs, b.sampled_trajs)
+    for s in parts:
+        s.eng.close()
+
+
 def multi_key(seed, c):
     from epipf import chain_key
     return chain_key(seed, c)

@@ -87,3 +87,32 @@ def test_cached_mvn_factor_equals_legacy_multivariate_normal(d):
             assert a_.shape == b_.shape == (d,)
             assert np.array_equal(a_, b_), (cov, a_, b_)
         assert ref.uniform() == mine.uniform()          # same stream position afterwards
+
+
+def test_pipelined_samplers_equal_one_lockstep_sampler(datasets_golden):
+    """run_pipelined (one host thread + private engine per chain group, bench.py --pipelines) gives every chain
+    exactly the draws, likelihoods and trajectories of one lockstep ChainSampler over all chains."""
+    from oracle_engine import OracleEngine
+    Y = datasets_golden["cfg1_binom"][:8]
+    kw = dict(Y=Y, type_model="sir", parameters=[2.0, 1.0], h=0.02, iters=7, probs=0.1, n_particles=16,
+              n_population=200, mu=20, mh_ratio="log")
+    ids = list(range(5))
+    whole = pm.ChainSampler(**kw, rngs=[np.random.RandomState(30 + g) for g in ids],
+                            keys=[pm.chain_key(30, g) for g in ids], engine=OracleEngine(0, 1, 16, 8, 5))
+    whole.initialise()
+    ran = sum(whole.step() for _ in range(6))
+    groups = [[0, 1], [2], [3, 4]]
+    parts = [pm.ChainSampler(**kw, rngs=[np.random.RandomState(30 + g) for g in grp],
+                             keys=[pm.chain_key(30, g) for g in grp], engine=OracleEngine(0, 1, 16, 8, len(grp)))
+             for grp in groups]
+    for s in parts:
+        s.initialise()
+    assert pm.run_pipelined(parts, 6) == ran
+    got = [r for s in parts for r in s.results()]
+    for a, b in zip(whole.results(), got):
+        np.testing.assert_array_equal(a.thetas, b.thetas)
+        np.testing.assert_array_equal(a.log_likelihoods, b.log_likelihoods)
+        np.testing.assert_array_equal(a.sampled_trajs, b.sampled_trajs)
+        assert a.acceptances == b.acceptances and a.filters_run == b.filters_run
+    with pytest.raises(ValueError):
+        pm.run_pipelined([parts[0], parts[0]], 1)
