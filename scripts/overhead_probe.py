@@ -18,7 +18,11 @@ eng = Engine("sir", 1, N, T, C, device=0)
 eng.set_observations(Y)
 eng.set_population(meta["n_population"], meta["mu"])
 Yc = np.tile(np.array([998.0, 2.0, 0.0]), (T, 1))       # observations the frozen initial states can explain
-for name, th in (("bench theta", meta["theta"]), ("no events", (0.0, 1e-12)), ("bench theta", meta["theta"])):
+cases = (("bench theta", meta["theta"]), ("no events", (0.0, 1e-12)), ("bench theta", meta["theta"]))
+only = os.environ.get("CASE")                                  # "bench" / "noev": one case (PMC passes)
+if only:
+    cases = [c for c in cases if (c[1][0] == 0.0) == (only == "noev")][:1]
+for name, th in cases:
     eng.set_observations(Yc if th[0] == 0.0 else Y)
     thetas = np.tile(np.asarray(th, dtype=np.float64), (C, 1))
     eng.run(thetas, meta["probs"], np.arange(C) + 7, 0)
