@@ -253,6 +253,12 @@ struct SsaState<kSIR, 1> {                                             // gilles
         return true;
     }
     __device__ __forceinline__ void save(double* x) const { x[0] = S; x[1] = I; x[2] = R + (double)nrec; }
+    // event()'s tau, same expressions (the wave-cooperative replay evaluates events' times in parallel)
+    __device__ __forceinline__ double tau_of(const Block& r, const ChainParam& cp, const LogTab* __restrict__ tab) const {
+        const double a0 = bN * (S * I);
+        const double as = fma(cp.theta[1], I, a0);
+        return recip(as) * neg_log_one_minus_u01(r.x, r.y, tab);
+    }
 };
 
 template <>
@@ -286,6 +292,11 @@ struct SsaState<kSEIR, 1> {                                            // gilles
         return true;
     }
     __device__ __forceinline__ void save(double* x) const { x[0] = S; x[1] = E; x[2] = I; x[3] = R; }
+    __device__ __forceinline__ double tau_of(const Block& r, const ChainParam& cp, const LogTab* __restrict__ tab) const {
+        const double a0 = bN * (S * I), a01 = fma(cp.theta[1], E, a0);
+        const double as = fma(cp.theta[2], I, a01);
+        return recip(as) * neg_log_one_minus_u01(r.x, r.y, tab);
+    }
 };
 
 template <int G>
@@ -350,6 +361,18 @@ struct SubgroupsState {                                                // gilles
     __device__ __forceinline__ void save(double* x) const {
 #pragma unroll
         for (int g = 0; g < G; ++g) { x[3 * g] = S[g]; x[3 * g + 1] = I[g]; x[3 * g + 2] = R[g]; }
+    }
+    __device__ __forceinline__ double tau_of(const Block& r, const ChainParam& cp, const LogTab* __restrict__ tab) const {
+        const double gamma = cp.theta[G * G];
+        double run = 0.0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const double cI = I[g] * invSumN;
+#pragma unroll
+            for (int g2 = 0; g2 < G; ++g2) run = fma(cp.theta[g * G + g2] * S[g2], cI, run);
+            run = fma(gamma, I[g], run);
+        }
+        return recip(run) * neg_log_one_minus_u01(r.x, r.y, tab);
     }
 };
 template <int G> struct SsaState<kSubgroups, G> : SubgroupsState<G> {};
@@ -552,14 +575,16 @@ template <int G> struct FastSsa<kSubgroups2, G> : FastSubgroups<G> {};
 
 template <int MODEL, int G>
 __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
-                                               double tmax, int& nev_out, int& iters) {
+                                               double tmax, int& nev_out, int& iters, bool& eligible) {
     using F = FastSsa<MODEL, G>;
     constexpr int NCH = F::NCH;
     iters = 0;
     nev_out = 0;
+    eligible = false;
     if (!(cp.flags & kChainFastSsa)) return false;
     F st;
     if (!st.load(x, cp)) return false;
+    eligible = true;
     double rem = tmax * kInvLn2;                                       // remaining time, units of 1/ln 2
     const float Bt = (float)rem * F::kClockT;
     float R = 0.f, df = 0.f, B = 0.f;
@@ -643,14 +668,116 @@ __device__ __forceinline__ int exact_propagate(double* x, const ChainParam& cp, 
     return nev;
 }
 
+// ------------------------------------------------------------------------------- wave-cooperative replay
+// A lane whose f32 loop ended too close to the step boundary to certify (|rem| <= B) needs the exact loop's answer,
+// and one lane running ~100 f64 events leaves 63 lanes idle.  The whole wave instead replays that particle in
+// chunks of 64 events:
+//   1. lane i computes event (base + i)'s Philox block (counter-based: independent of the state);
+//   2. one uniform pass applies the chunk's channel decisions in order -- the f32 loop's certified test with the
+//      exact fallback, which is the exact loop's decision -- and lane i keeps the state before event base + i;
+//   3. lane i evaluates that event's time with the exact loop's expressions (SsaState::tau_of);
+//   4. one uniform pass adds the times in event order (t + tau > tmax ends the step, as the exact loop's test).
+// The result is the exact loop's, bit for bit (tests/test_gpu_parity.py: EPIPF_SSA_FAST=0 vs 1), at ~20 wave
+// instructions per event instead of ~130.  Requires every lane of the wave (call it with full exec).
+template <typename F>
+__device__ __forceinline__ int fast_channel(const F& st, const ChainParam& cp, uint32_t rz, uint32_t rw) {
+    constexpr int NCH = F::NCH;
+    float c[NCH - 1];
+    const float total = st.cum(c);
+    const float ri = __builtin_amdgcn_rcpf(total);
+    const float uc = __uint_as_float(0x3F800000u | (rw >> 9)) - (1.0f - kUlpF);
+    bool close = false;
+    int ch = 0;
+    if constexpr (NCH <= 3) {
+#pragma unroll
+        for (int i = 0; i < NCH - 1; ++i) {
+            const float q = c[i] * ri;
+            ch += (q < uc) ? 1 : 0;
+            close |= fabsf(q - uc) <= F::kBand;
+        }
+    } else {
+        const float T = uc * total, band = F::kBand * total;
+#pragma unroll
+        for (int i = 0; i < NCH - 1; ++i) {
+            ch += (c[i] < T) ? 1 : 0;
+            close |= fabsf(c[i] - T) <= band;
+        }
+    }
+    if (close) ch = st.exact_channel(cp, u01(rz, rw));
+    return ch;
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const uint64_t b = __double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, lane), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), lane);
+    return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+
+template <int MODEL, int G>
+__device__ __forceinline__ int coop_replay(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag, double tmax,
+                                        const LogTab* __restrict__ tab) {
+    using F = FastSsa<MODEL, G>;
+    constexpr int C = (MODEL == kSIR) ? 3 : (MODEL == kSEIR) ? 4 : 3 * G;
+    const int lane = (int)(threadIdx.x & 63);
+    F st;
+    st.load(x, cp);                                      // eligible: the f32 loop ran on this particle
+    double t = 0.0;
+    uint32_t base = 0;
+    int nev = 0;
+    bool more = st.active();
+    while (more) {
+        const Block r = philox(base + (uint32_t)lane, j, ptag, cp.f, cp.k0, cp.k1);
+        F mine = st;                                     // state before event base + lane
+        int nk = 64;                                     // events of this chunk up to extinction
+        for (int i = 0; i < 64; ++i) {
+            if (lane == i) mine = st;
+            const uint32_t rz = __builtin_amdgcn_readlane(r.z, i), rw = __builtin_amdgcn_readlane(r.w, i);
+            st.apply(fast_channel(st, cp, rz, rw), 1.f);
+            if (!st.active()) { nk = i + 1; break; }
+        }
+        double tau = 0.0;
+        if (lane < nk) {
+            double xk[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) xk[c] = x[c];
+            mine.save(xk);
+            SsaState<MODEL, G> ex;
+            ex.load(xk, cp);
+            tau = ex.tau_of(r, cp, tab);
+        }
+        int stop = -1;                                   // first event of the chunk past tmax
+        for (int i = 0; i < nk; ++i) {
+            const double tn = t + readlane_f64(tau, i);
+            if (tn > tmax) { stop = i; break; }
+            t = tn;
+        }
+        if (stop >= 0) {                                 // the step ends before event base + stop
+            nev += stop;
+            double xs[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) xs[c] = x[c];
+            mine.save(xs);
+#pragma unroll
+            for (int c = 0; c < C; ++c) x[c] = readlane_f64(xs[c], stop);
+            return nev;
+        }
+        nev += nk;
+        base += 64u;
+        more = nk == 64;                                 // else the population died out after the last event
+    }
+    st.save(x);
+    return nev;
+}
+
 // One particle over [0, tmax]: the certified f32 path first; lanes it cannot certify run the exact loop from the
 // untouched parent state.
 template <int MODEL, int G>
 __device__ __forceinline__ int ssa_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
                                              double tmax, const LogTab* __restrict__ tab, int& iters, int& exact) {
     int fast_iters = 0, fast_nev = 0;
+    bool eligible = false;
     exact = 1;
-    if (fast_propagate<MODEL, G>(x, cp, j, ptag, tmax, fast_nev, fast_iters)) {
+    if (fast_propagate<MODEL, G>(x, cp, j, ptag, tmax, fast_nev, fast_iters, eligible)) {
         iters = fast_iters;
         exact = 0;
         return fast_nev;
@@ -843,12 +970,6 @@ __device__ __forceinline__ int resample_search_seg(double U, const double* seg_s
     certified = (va - cert_halfwidth(a, va, cert_k) > U) &&
                 (a == 0 || vp + cert_halfwidth(a - 1, vp, cert_k) < U) && a < N;
     return a;
-}
-
-__device__ __forceinline__ double readlane_f64(double x, int l) {
-    const long long b = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-    return __hiloint2double(hi, lo);
 }
 
 // The exact reference draw for every lane of the wave with need == true, all 64 lanes cooperating (call

@@ -190,23 +190,41 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
 #pragma unroll
     for (int c = 0; c < C; ++c) x[c] = 0.0;
     const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
-    bool fast_ok = false;
+    bool fast_ok = false, eligible = false;
     if (j < a.N) {
         anc = min(max(anc, 0), a.N - 1);
         a.ancestry[(size_t)chain * a.anc_stride + (size_t)p * a.N + j] = anc;   // :193
         const int32_t* hp = a.hidden + (size_t)chain * a.hist_stride + ((size_t)(p - 1) * a.N + anc) * C;
 #pragma unroll
         for (int c = 0; c < C; ++c) x[c] = (double)hp[c];
-        fast_ok = fast_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, nev, iters);
+        fast_ok = fast_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, nev, iters, eligible);
     }
     exact = (j < a.N && !fast_ok) ? 1 : 0;
     if (__any(exact != 0)) {
         for (int i = tid; i < kLogTabEntries; i += WG) tab[i] = a.logtab[i];
         __syncthreads();
-        if (exact) {
+        // lanes the f32 loop could not run (population or rates out of its range): the exact loop, per lane
+        // (the subgroup models keep the per-lane exact loop: the inlined replay would cost them occupancy)
+        constexpr bool kCoop = MODEL == kSIR || MODEL == kSEIR;
+        if (exact && (!eligible || !kCoop)) {
             int ex_iters = 0;
             nev = exact_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, tab, ex_iters);
             iters += ex_iters;
+        }
+        // lanes it stopped at the step boundary: replayed one at a time by the whole wave (coop_replay)
+        unsigned long long pend = kCoop ? __ballot(exact != 0 && eligible) : 0ull;
+        while (pend) {
+            const int L = (int)__builtin_ctzll(pend);
+            pend &= pend - 1ull;
+            double xl[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) xl[c] = readlane_f64(x[c], L);
+            const int n = coop_replay<MODEL, G>(xl, cp, __builtin_amdgcn_readlane((uint32_t)j, L), ptag, 1.0, tab);
+            if (tid == L) {
+#pragma unroll
+                for (int c = 0; c < C; ++c) x[c] = xl[c];
+                nev = n;
+            }
         }
     }
     if (j < a.N) {
