@@ -390,7 +390,8 @@ template <int G> struct SsaState<kSubgroups2, G> : SubgroupsState<G> {};
 //            error drops out: 2 e_as + 2 ulp, inside the same band).
 //   clock    time is kept in units of 1/ln 2 and counted down: rem = tmax/ln2 + sum(log2(x_f) * rcp(total)),
 //            the event is inside the step iff rem >= 0 (the exact path's t + tau <= tmax, scaled).  x_f = 1 - U
-//            from two converts (relative error <= 3 ulp for x >= 2^-20); v_log_f32 is within 2 ulp of |log2 x|
+//            from its top word for x >= 2^-8 (one convert, scaled exactly: the convert's rounding plus the dropped
+//            low word, <= 2 ulp), from two converts below (<= 3 ulp for x >= 2^-20); v_log_f32 is within 2 ulp of |log2 x|
 //            on every float in [2^-20, 1) (exhaustive, scripts/f32_accuracy.hip); below 2^-20 (2^-20 of events)
 //            log2 is taken in f64 of the exact x and rounded (tiny_log2, <= 0.5 ulp + 2^-29).  Per event
 //            |tau2_f - tau2| <= (e_as + 5.5) ulp |tau2_f| + 4.4 ulp rcp(total), so with R = sum rcp(total) the
@@ -620,9 +621,11 @@ __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, 
         }
         if (close) ch = st.exact_channel(cp, u01(r.z, r.w));
         const uint32_t nh = ~r.y;
-        float lg;
-        if (nh < 4096u) lg = tiny_log2(~r.x, r.y);                    // 1 - U < 2^-20: 2^-20 of events
-        else lg = __builtin_amdgcn_logf(fmaf((float)nh, 0x1.0p-32f, (float)r.x * 0x1.0p-64f));  // 1 - U (r.x is ~x)
+        float lg = __builtin_amdgcn_logf((float)nh * 0x1.0p-32f);     // 1 - U from its top word: <= 2 ulp for x >= 2^-8
+        if (nh < 0x1000000u) {                                         // 1 - U < 2^-8: 0.4% of events
+            if (nh < 4096u) lg = tiny_log2(~r.x, r.y);                // 1 - U < 2^-20
+            else lg = __builtin_amdgcn_logf(fmaf((float)nh, 0x1.0p-32f, (float)r.x * 0x1.0p-64f));  // r.x is ~x
+        }
         rem = rem + (double)(lg * ri);                                 // np.random.exponential
         R += ri;
         df = (float)rem;
