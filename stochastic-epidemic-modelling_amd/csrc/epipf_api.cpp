@@ -88,6 +88,7 @@ struct epipf_ctx {
     void* abc = nullptr;
     bool abc_order = true;   // length-ordered ABC lanes (EPIPF_ABC_ORDER=0 disables)
     bool fast_ssa = true;    // certified f32 event loop (EPIPF_SSA_FAST=0 disables; results are identical)
+    float clock_slack = 1.f; // EPIPF_CLOCK_SLACK >= 1 widens its clock band: replays on purpose (stress tests)
     int n_streams = 4;   // chain groups on concurrent streams (EPIPF_STREAMS overrides, 1..kMaxFilterStreams)
     hipStream_t aux[kMaxFilterStreams] = {};
     hipEvent_t join[kMaxFilterStreams] = {};
@@ -178,6 +179,7 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     c->max_chains = max_chains;
     c->wg = default_wg(n_particles);
     if (const char* e = getenv("EPIPF_SSA_FAST")) c->fast_ssa = atoi(e) != 0;
+    if (const char* e = getenv("EPIPF_CLOCK_SLACK")) c->clock_slack = std::max(1.0f, std::min(1e6f, (float)atof(e)));
     if (const char* e = getenv("EPIPF_STREAMS")) c->n_streams = std::max(1, std::min(kMaxFilterStreams, atoi(e)));
     c->B = (n_particles + c->wg - 1) / c->wg;
     if (step_lds_bytes(c->B, c->wg) > 160 * 1024) {
@@ -308,6 +310,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
         q.k1 = (uint32_t)(keys[ch] >> 32);
         q.f = filter_index[ch];
         q.flags = c->fast_ssa ? kChainFastSsa : 0u;
+        q.clock_slack = c->clock_slack;
         c->h_status[ch] = on ? EPIPF_STATUS_OK : EPIPF_STATUS_SKIPPED;
         n_active += on;
     }
@@ -471,6 +474,7 @@ int epipf_simulate(epipf_ctx* c, int n, const int32_t* states_in, const double* 
     for (int i = 0; i < d; ++i) { q.theta[i] = theta[i]; q.thetaf[i] = (float)theta[i]; }
     q.k0 = (uint32_t)key; q.k1 = (uint32_t)(key >> 32); q.f = filter_index;
     q.flags = c->fast_ssa ? kChainFastSsa : 0u;
+    q.clock_slack = c->clock_slack;
     HIP_TRY(hipMemcpyAsync(dcp, &q, sizeof q, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(din, states_in, sizeof(int32_t) * (size_t)n * c->C, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(dev_events, 0, sizeof(unsigned long long), c->stream));

@@ -79,6 +79,7 @@ struct ChainParam {
     uint32_t f;                // filter index
     uint32_t flags;            // kChainFastSsa: the certified f32 event loop may run (EPIPF_SSA_FAST=0 clears it)
     float thetaf[kMaxTheta];   // theta rounded to f32 on the host (scalar loads: the fast path's rates stay in SGPRs)
+    float clock_slack;         // >= 1: widens the f32 loop's clock band (more replays, same results); tests only
 };
 constexpr uint32_t kChainFastSsa = 1u;   // (all models)
 
@@ -587,7 +588,7 @@ __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, 
     if (!st.load(x, cp)) return false;
     eligible = true;
     double rem = tmax * kInvLn2;                                       // remaining time, units of 1/ln 2
-    const float Bt = (float)rem * F::kClockT;
+    const float Bt = (float)rem * F::kClockT * cp.clock_slack;
     float R = 0.f, df = 0.f, B = 0.f;
     uint32_t ks = 0;                                                   // event index, wave-uniform (SGPR)
     bool alive = st.active(), ok = true;

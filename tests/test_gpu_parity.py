@@ -391,19 +391,59 @@ def test_full_size_cfg2_properties(datasets_golden):
     np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-8)
 
 
-def _engine_with_fast_ssa(enabled, N, T, chains, model="sir", groups=1):
-    """A fresh context with the certified f32 event loop on or off (EPIPF_SSA_FAST is read at create)."""
+def _engine_with_fast_ssa(enabled, N, T, chains, model="sir", groups=1, slack=None):
+    """A fresh context with the certified f32 event loop on or off (EPIPF_SSA_FAST is read at create), and
+    optionally its clock band widened `slack` times (EPIPF_CLOCK_SLACK: more replays, same results)."""
     import os
     from epipf.engine import Engine
-    old = os.environ.get("EPIPF_SSA_FAST")
-    os.environ["EPIPF_SSA_FAST"] = "1" if enabled else "0"
+    env = {"EPIPF_SSA_FAST": "1" if enabled else "0", "EPIPF_CLOCK_SLACK": None if slack is None else str(slack)}
+    old = {k: os.environ.get(k) for k in env}
+    for k, v in env.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
     try:
         return Engine(model, groups, N, T, chains)
     finally:
-        if old is None:
-            del os.environ["EPIPF_SSA_FAST"]
-        else:
-            os.environ["EPIPF_SSA_FAST"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("model,groups,ds,theta,npop,obs", [
+    ("sir", 1, "cfg2_binom", [[0.25, 0.1], [0.5, 0.2], [0.3, 0.05]], 10000.0, False),
+    ("seir", 1, "cfg3_noisy", [[0.5, 0.2, 0.1], [0.9, 0.3, 0.2], [0.4, 0.2, 0.05]], 10000.0, True),
+    ("sir_subgroups", 2, "sub_binom", [[5.0, 2.0, 1.0, 3.0, 0.5], [4.0, 2.0, 1.0, 3.0, 0.5], [5.0, 1.5, 1.0, 2.5, 0.6]],
+     [2030.0, 3040.0], False),
+])
+@pytest.mark.parametrize("slack", [300, 30000])
+def test_replays_on_purpose_equal_exact_path(datasets_golden, model, groups, ds, theta, npop, obs, slack):
+    """Stress the replay path: the f32 loop's clock band widened 300x / 30000x hands a large share of particle-steps
+    to the replay (the wave-cooperative one for SIR / SEIR, the per-lane exact loop for subgroups); states,
+    ancestors and likelihoods stay bit-identical to the exact loop's."""
+    Y = datasets_golden[ds][:40]
+    N, T, C = 3000, Y.shape[0], len(theta)
+    th = np.array(theta)
+    out = []
+    for fast, sl in ((True, slack), (False, None)):
+        eng = _engine_with_fast_ssa(fast, N, T, C, model=model, groups=groups, slack=sl)
+        eng.set_observations(Y)
+        eng.set_population(npop, [30.0, 40.0] if groups > 1 else 20.0)
+        eng.set_profiling(2)
+        lz, st = eng.run(th, [0.1] * C, [31 + c for c in range(C)], [2] * C, observations=obs)
+        hid, anc = eng.history(C)
+        out.append((lz, st, hid, anc, eng.stats()))
+        eng.close()
+    (lz1, st1, h1, a1, s1), (lz0, st0, h0, a0, s0) = out
+    np.testing.assert_array_equal(st1, st0)
+    np.testing.assert_array_equal(h1, h0)
+    np.testing.assert_array_equal(a1, a0)
+    np.testing.assert_array_equal(lz1, lz0)
+    assert s1["events"] == s0["events"]
+    assert s1["ssa_exact_lanes"] > (0.002 if slack == 300 else 0.3) * s1["particle_steps"]
 
 
 def test_fast_ssa_path_equals_exact_path_at_scale(datasets_golden):
