@@ -518,3 +518,33 @@ def test_fast_ssa_path_equals_exact_path_other_models(datasets_golden, model, gr
     np.testing.assert_array_equal(a1, a0)
     np.testing.assert_array_equal(lz1, lz0)
     assert s1["events"] == s0["events"] and s1["ssa_exact_lanes"] < s0["ssa_exact_lanes"]
+
+
+@pytest.mark.parametrize("model,T,N,mu", [("sir", 1, 65, 20.0), ("sir", 2, 1, 20.0), ("sir", 3, 500, 20.0),
+                                          ("seir", 2, 130, 20.0), ("sir", 6, 300, 0.0), ("sir_subgroups", 2, 64, 20.0),
+                                          ("sir_subgroups2", 3, 200, 0.0)])
+def test_filter_short_horizons_and_extinct_starts_vs_oracle(datasets_golden, model, T, N, mu):
+    """Edge shapes: T = 1 (init only, no step kernel), T = 2 / 3, a single particle, and mu = 0 (every initial
+    infected count 0: no SSA event anywhere); bit-exact vs the oracle."""
+    if model == "sir":
+        Y, th, npop = datasets_golden["sir_binom"][:T], (2.0, 1.0), 4820.0
+    elif model == "seir":
+        Y, th, npop = datasets_golden["seir_binom"][:T], (4.0, 1.0, 1.0), 4820.0
+    else:
+        Y = datasets_golden["sub_binom" if model == "sir_subgroups" else "sub2_binom"][:T]
+        th, npop = (np.array([[5.0, 2.0], [1.0, 3.0]]), 0.5), np.array([2030.0, 3040.0])
+    mus = np.array([mu, mu]) if model.startswith("sir_sub") else mu
+    if mu == 0.0:                                   # nobody infected: observations of I and R are 0 (weights > 0)
+        Y = Y.copy()
+        Y[:, 1:] = 0.0
+    a = dict(Y=Y, model=model, theta=th, N=N, npop=npop, mu=mus)
+    eng, thv = engine_for(a)
+    lz, st = eng.run(thv[None], [0.1], [123], [4])
+    o = oracle.particle_filter(Y, model, th, False, 0.1, N, npop, mus, key=123, filter_index=4)
+    assert int(st[0]) == o["status"]
+    if o["status"]:
+        return
+    hid, anc = eng.history(1)
+    np.testing.assert_array_equal(hid[0], o["hidden"])
+    np.testing.assert_array_equal(anc[0], o["ancestry"])
+    np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
