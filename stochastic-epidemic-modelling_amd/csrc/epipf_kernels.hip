@@ -204,8 +204,9 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
         for (int i = tid; i < kLogTabEntries; i += WG) tab[i] = a.logtab[i];
         __syncthreads();
         // lanes the f32 loop could not run (population or rates out of its range): the exact loop, per lane
-        // (the subgroup models keep the per-lane exact loop: the inlined replay would cost them occupancy)
-        constexpr bool kCoop = MODEL == kSIR || MODEL == kSEIR;
+        // Subgroups with G <= 2 too, although the inlined replay costs that kernel occupancy (69 -> 91 VGPRs, 7 -> 5
+        // waves per SIMD): with 5-6x the events per step, its replays dominate (cfg5 +13.6%).  G >= 3: exact loop.
+        constexpr bool kCoop = MODEL == kSIR || MODEL == kSEIR || G <= 2;
         if (exact && (!eligible || !kCoop)) {
             int ex_iters = 0;
             nev = exact_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, tab, ex_iters);
