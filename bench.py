@@ -215,7 +215,10 @@ def main():
                 peak = 1024 * 2.4e9 / 2
                 valu = {"achieved": per_ps * value, "peak": peak, "unit": "wave64 VALU instr/s",
                         "frac": per_ps * value / peak, "instr_per_particle_step": per_ps,
-                        "cycles_per_instr_at_2.4GHz": 1024 * 2.4e9 / (per_ps * value)}
+                        "cycles_per_instr_at_2.4GHz": 1024 * 2.4e9 / (per_ps * value),
+                        # VALU pipe busy per SIMD-cycle, SQ_ACTIVE_INST_VALU / GRBM_GUI_ACTIVE of the PMC pass
+                        # (dispatches serialised there, so each carries its own launch tail)
+                        "pmc_valu_busy_frac": pmc.get("valu_busy_frac")}
         except (OSError, ValueError):
             traffic = None
     # SSA events per second of job time: events per particle-step (counters iteration) x the measured rate

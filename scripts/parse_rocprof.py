@@ -59,6 +59,13 @@ def main(d):
         lanes = float(meta.get("Grid_Size") or 0)
         if lanes > 0:
             out["hbm_bytes_per_particle_step"] = raw / lanes
+    # VALU pipe utilisation (the bound of this kernel): SQ_ACTIVE_INST_VALU counts quad-cycles of VALU
+    # execution summed over waves, GRBM_GUI_ACTIVE GPU cycles summed over the 8 XCDs (MI355X_MICROARCH.md), both
+    # in the same pass, over the 1024 SIMDs; dispatches are serialised under counter collection
+    act, gui = per.get("SQ_ACTIVE_INST_VALU", {}), per.get("GRBM_GUI_ACTIVE", {})
+    both = [k for k in act if k in gui]
+    if both:
+        out["valu_busy_frac"] = 4.0 * sum(act[k] for k in both) / (1024.0 * sum(gui[k] for k in both) / 8.0)
     lanes = float(meta.get("Grid_Size") or 0)
     if lanes > 0:   # one lane per particle (padding of the last block included: < 0.5% at N = 10^4)
         out["particle_steps_per_launch"] = lanes
