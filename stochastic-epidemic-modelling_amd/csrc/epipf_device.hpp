@@ -717,21 +717,29 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
     return __longlong_as_double(((uint64_t)hi << 32) | lo);
 }
 
+// row: the particle's output row, holding its parent state on entry and its new state on return (every lane reads
+// it; the state is not kept in registers across the replay).
 template <int MODEL, int G>
-__device__ __forceinline__ int coop_replay(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag, double tmax,
-                                        const LogTab* __restrict__ tab) {
+__device__ __forceinline__ int coop_replay(int32_t* row, const ChainParam& cp, uint32_t j, uint32_t ptag, double tmax,
+                                           const LogTab* __restrict__ tab) {
     using F = FastSsa<MODEL, G>;
     constexpr int C = (MODEL == kSIR) ? 3 : (MODEL == kSEIR) ? 4 : 3 * G;
     const int lane = (int)(threadIdx.x & 63);
     F st;
-    st.load(x, cp);                                      // eligible: the f32 loop ran on this particle
+    {
+        double x0[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) x0[c] = (double)row[c];
+        st.load(x0, cp);                                 // eligible: the f32 loop ran on this particle
+    }
     double t = 0.0;
     uint32_t base = 0;
     int nev = 0;
     bool more = st.active();
+    F mine = st;                                         // state before event base + lane
     while (more) {
         const Block r = philox(base + (uint32_t)lane, j, ptag, cp.f, cp.k0, cp.k1);
-        F mine = st;                                     // state before event base + lane
+        mine = st;
         int nk = 64;                                     // events of this chunk up to extinction
         for (int i = 0; i < 64; ++i) {
             if (lane == i) mine = st;
@@ -743,7 +751,7 @@ __device__ __forceinline__ int coop_replay(double* x, const ChainParam& cp, uint
         if (lane < nk) {
             double xk[C];
 #pragma unroll
-            for (int c = 0; c < C; ++c) xk[c] = x[c];
+            for (int c = 0; c < C; ++c) xk[c] = (double)row[c];
             mine.save(xk);
             SsaState<MODEL, G> ex;
             ex.load(xk, cp);
@@ -759,17 +767,31 @@ __device__ __forceinline__ int coop_replay(double* x, const ChainParam& cp, uint
             nev += stop;
             double xs[C];
 #pragma unroll
-            for (int c = 0; c < C; ++c) xs[c] = x[c];
+            for (int c = 0; c < C; ++c) xs[c] = (double)row[c];
             mine.save(xs);
+            int32_t v[C];
 #pragma unroll
-            for (int c = 0; c < C; ++c) x[c] = readlane_f64(xs[c], stop);
+            for (int c = 0; c < C; ++c) v[c] = (int32_t)readlane_f64(xs[c], stop);
+            __syncthreads();                             // every lane has read the parent row
+            if (lane == 0) {
+#pragma unroll
+                for (int c = 0; c < C; ++c) row[c] = v[c];
+            }
             return nev;
         }
         nev += nk;
         base += 64u;
         more = nk == 64;                                 // else the population died out after the last event
     }
-    st.save(x);
+    double xf[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) xf[c] = (double)row[c];
+    st.save(xf);
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) row[c] = (int32_t)xf[c];
+    }
     return nev;
 }
 

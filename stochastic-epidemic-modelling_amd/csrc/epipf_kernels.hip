@@ -204,27 +204,32 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
         for (int i = tid; i < kLogTabEntries; i += WG) tab[i] = a.logtab[i];
         __syncthreads();
         // lanes the f32 loop could not run (population or rates out of its range): the exact loop, per lane
-        // Subgroups with G <= 2 too, although the inlined replay costs that kernel occupancy (69 -> 91 VGPRs, 7 -> 5
-        // waves per SIMD): with 5-6x the events per step, its replays dominate (cfg5 +13.6%).  G >= 3: exact loop.
-        constexpr bool kCoop = MODEL == kSIR || MODEL == kSEIR || G <= 2;
-        if (exact && (!eligible || !kCoop)) {
+        if (exact && !eligible) {
             int ex_iters = 0;
             nev = exact_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, tab, ex_iters);
             iters += ex_iters;
         }
-        // lanes it stopped at the step boundary: replayed one at a time by the whole wave (coop_replay)
-        unsigned long long pend = kCoop ? __ballot(exact != 0 && eligible) : 0ull;
-        while (pend) {
-            const int L = (int)__builtin_ctzll(pend);
-            pend &= pend - 1ull;
-            double xl[C];
+        // lanes it stopped at the step boundary: replayed one at a time by the whole wave (coop_replay).  The lanes'
+        // states wait in their output rows meanwhile (x is not live across the replay: registers, occupancy).
+        unsigned long long pend = __ballot(exact != 0 && eligible);
+        if (pend) {
+            int32_t* hrow = a.hidden + (size_t)chain * a.hist_stride + (size_t)p * a.N * C;
+            if (j < a.N) {
 #pragma unroll
-            for (int c = 0; c < C; ++c) xl[c] = readlane_f64(x[c], L);
-            const int n = coop_replay<MODEL, G>(xl, cp, __builtin_amdgcn_readlane((uint32_t)j, L), ptag, 1.0, tab);
-            if (tid == L) {
+                for (int c = 0; c < C; ++c) hrow[(size_t)j * C + c] = (int32_t)x[c];   // replayed lanes: the parent
+            }
+            __syncthreads();                                          // one wave per block: orders the rows
+            while (pend) {
+                const int L = (int)__builtin_ctzll(pend);
+                pend &= pend - 1ull;
+                const uint32_t jl = __builtin_amdgcn_readlane((uint32_t)j, L);
+                const int n = coop_replay<MODEL, G>(hrow + (size_t)jl * C, cp, jl, ptag, 1.0, tab);
+                if (tid == L) nev = n;
+            }
+            __syncthreads();
+            if (j < a.N) {
 #pragma unroll
-                for (int c = 0; c < C; ++c) x[c] = xl[c];
-                nev = n;
+                for (int c = 0; c < C; ++c) x[c] = (double)hrow[(size_t)j * C + c];
             }
         }
     }
