@@ -183,9 +183,9 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
             atomicAdd(counter_slot(a.counters) + 1, 1ull);
         }
     }
-    // (f) gather the parent state, (g) propagate over [0, 1], :195-220: the certified f32 loop, then the exact loop
-    // for the lanes it hands back.  The exact loop's log table is copied to LDS only by waves that need it (~1.5%
-    // at config 2): one wave per block, so the wave-uniform test is block-uniform and the barrier is legal.
+    // (f) gather the parent state, (g) propagate over [0, 1], :195-220: the certified f32 loop, then the exact path
+    // for the lanes it hands back.  The exact path's log table is copied to LDS only by waves that need it (~1% at
+    // config 2): one wave per block, so the wave-uniform test is block-uniform and the barriers are legal.
     double x[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) x[c] = 0.0;
