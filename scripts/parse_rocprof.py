@@ -59,6 +59,7 @@ def main(d):
         lanes = float(meta.get("Grid_Size") or 0)
         if lanes > 0:
             out["hbm_bytes_per_particle_step"] = raw / lanes
+            out["hbm_bytes_per_particle_step_read_doubled"] = out["hbm_bytes_per_launch_read_doubled"] / lanes
     # VALU pipe utilisation (the bound of this kernel): SQ_ACTIVE_INST_VALU counts quad-cycles of VALU
     # execution summed over waves, GRBM_GUI_ACTIVE GPU cycles summed over the 8 XCDs (MI355X_MICROARCH.md), both
     # in the same pass, over the 1024 SIMDs; dispatches are serialised under counter collection
