@@ -65,7 +65,7 @@ class _Stream:
                 self.snaps[n] = self.rs.get_state()
             self.z.append(self.rs.standard_normal(self.d))
             self.chosen.append(self.rs.randint(0, self.N))
-            self.u.append(self.rs.uniform())
+            self.u.append(self.rs.random_sample())           # == uniform() (0 + 1*U), same draw
         return self.z[k], self.chosen[k], self.u[k]
 
     def fork(self, k):
@@ -80,7 +80,7 @@ class _Stream:
             for _ in range(k - k0):
                 rs.standard_normal(self.d)
                 rs.randint(0, self.N)
-                rs.uniform()
+                rs.random_sample()
             rs.standard_normal(self.d)
             f = self.forks[k] = _Stream(rs.get_state(), self.d, self.N)
         return f
@@ -250,7 +250,7 @@ class PrefetchSampler(ChainSampler):
         rng.standard_normal(self.d)                             # the proposal's normals (multivariate_normal)
         if filtered and x.result[1] == _lib.STATUS_OK:
             rng.randint(0, self.N)                              # path pick, pmcmc.py:241
-            rng.uniform()                                       # acceptance uniform, :395
+            rng.random_sample()                                 # acceptance uniform (== uniform()), :395
         i = x.i
         z, lz, traj = _value(y.src)
         self.thetas[c, i] = y.theta

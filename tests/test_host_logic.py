@@ -116,3 +116,17 @@ def test_pipelined_samplers_equal_one_lockstep_sampler(datasets_golden):
         assert a.acceptances == b.acceptances and a.filters_run == b.filters_run
     with pytest.raises(ValueError):
         pm.run_pipelined([parts[0], parts[0]], 1)
+
+
+def test_random_sample_is_legacy_uniform():
+    """The MH acceptance draw (pmcmc.py:395, np.random.uniform()) is taken as random_sample(): legacy uniform is
+    low + (high - low) * random_sample() = 0 + 1 * U, the same double and the same stream consumption."""
+    a, b = np.random.RandomState(9), np.random.RandomState(9)
+    for _ in range(20000):
+        assert a.uniform() == b.random_sample()
+        a.standard_normal(2), b.standard_normal(2)
+    assert a.randint(0, 1000) == b.randint(0, 1000)
+    np.random.seed(4)
+    x = np.random.uniform()
+    np.random.seed(4)
+    assert np.random.random_sample() == x
