@@ -25,6 +25,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "stochastic-epidemic-modelling_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters
+VALU_PEAK = 1024 * 2.4e9 / 2   # wave64 VALU instructions/s: 1024 SIMDs, 2.4 GHz, one wave64 instruction per 2 cycles
+MODEL_NAMES = {"sir": "SIR", "seir": "SEIR", "sir_subgroups": "multi-subgroup SIR", "sir_subgroups2": "SIR subgroups2"}
 
 
 def parse():
@@ -59,32 +61,68 @@ def cpu_model():
     return platform.processor()
 
 
+def host_threads():
+    """CPU threads this process may use: the box's allotment (OMP_NUM_THREADS is set to it on the GPU box; the
+    machine's full CPU count, os.cpu_count(), is many times that), else the affinity mask."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(avail, int(env))) if env and env.isdigit() else avail
+
+
 def cpu_baseline(Y, meta, N, seconds):
-    """Oracle (C restatement of the reference filter, OpenMP over particles) on the GPU box's host.
-    Sample: whole cfg filters (N particles x T steps) repeated until `seconds` elapse (at least one)."""
+    """The oracle (C restatement of the reference filter, OpenMP over particles) on the GPU box's host, at 1 thread
+    and at every thread this process is allotted.  Sample: whole filters of the bench config (N particles x T
+    steps) repeated until `seconds` elapse (at least one) per thread count.  The reference itself never runs on the
+    GPU box: scripts/time_reference.py times it in the build container next to the same port, and the
+    port/reference factor it measured (profiles/r2_reference_timing.json) converts the port's rates into the
+    reference's (`reference_calibrated`)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
-    threads = min(16, os.cpu_count() or 1)
-    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
     oracle.build()
     th = np.array(meta["theta"], dtype=np.float64)
     if meta["model"].startswith("sir_subgroups"):                     # (beta[G][G], gamma), pmcmc.py:289-296
         G = int(round(np.sqrt(th.size - 1)))
         th = (th[:G * G].reshape(G, G), th[-1])
-    t0 = time.perf_counter()
-    n = 0
-    ev = 0
-    while True:
-        o = oracle.particle_filter(Y, meta["model"], th, meta.get("observations", False), meta["probs"], N,
-                                   meta["n_population"], meta["mu"], key=7, filter_index=n)
-        n += 1
-        ev += o["events"]
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    return dict(value=n * N * Y.shape[0] / dt, unit="particle-steps/s", cores=oracle.num_threads(), kind="port",
-                sample=f"{n} full filter(s) of the bench config (N={N}, T={Y.shape[0]}), {dt:.1f}s, {ev / dt:.3g} events/s, "
-                       f"host CPU: {cpu_model()}")
+
+    def timed(threads, budget):
+        oracle.set_num_threads(threads)
+        t0 = time.perf_counter()
+        n = ev = 0
+        while True:
+            o = oracle.particle_filter(Y, meta["model"], th, meta.get("observations", False), meta["probs"], N,
+                                       meta["n_population"], meta["mu"], key=7, filter_index=n)
+            n += 1
+            ev += o["events"]
+            if time.perf_counter() - t0 >= budget:
+                break
+        dt = time.perf_counter() - t0
+        return n, dt, ev, oracle.num_threads()
+
+    allt = host_threads()
+    n, dt, ev, used = timed(allt, seconds)
+    n1, dt1, ev1, _ = timed(1, seconds)
+    value, value1 = n * N * Y.shape[0] / dt, n1 * N * Y.shape[0] / dt1
+    base = dict(value=value, unit="particle-steps/s", cores=used, kind="port",
+                sample=f"{n} full filter(s) of the bench config (N={N}, T={Y.shape[0]}) on {used} threads in {dt:.1f}s "
+                       f"({ev / dt:.3g} events/s); host CPU: {cpu_model()}, {used} threads allotted to this process of "
+                       f"{os.cpu_count()} on the machine",
+                single_core={"value": value1, "cores": 1, "sample": f"{n1} full filter(s) in {dt1:.1f}s",
+                             "events_per_s": ev1 / dt1})
+    cal_path = os.path.join(REPO, "profiles", "r2_reference_timing.json")
+    if os.path.exists(cal_path) and meta["model"] == "sir":
+        cal = json.load(open(cal_path))
+        f1 = cal["factor_port_over_reference_1core"]
+        base["reference_calibrated"] = {
+            "reference_1core_value": value1 / f1,
+            "factor_port_over_reference_1core": f1,
+            "reference_measured": {k: v["particle_steps_per_s"] for k, v in cal["reference"].items()},
+            "reference_host": f"{cal['host_cpu']} ({cal['host_cpus']} CPUs), build container",
+            "source": "profiles/r2_reference_timing.json (scripts/time_reference.py: unmodified reference "
+                      "particle_filter, jobs=1 / jobs=-1, config 2 data)"}
+    return base
 
 
 def main():
@@ -181,6 +219,12 @@ def main():
     else:
         filters_all = filters
     value = filters_all * N * T / dt
+    # Gelman-Rubin R-hat of every chain's gathered draws (helpers.py:15-43), outside the timed region
+    from epipf.chains_io import gelman_rubin
+    from epipf.distributed import unpack_draws
+    d_par = samplers[0].d
+    g_th, _ = unpack_draws(gathered, d_par)
+    rhat = gelman_rubin(list(g_th)) if g_th.shape[0] >= 2 and g_th.shape[1] >= 2 else None
 
     # roofline of the dominant kernel: pf_step_kernel (resample + gather + SSA + weight + in-block scan)
     # One filter step of every chain on this rank is issued as `streams` concurrent pf_step_kernel launches, one
@@ -193,38 +237,47 @@ def main():
     units_per_launch = filters * N / args.steps / streams            # particle-steps per kernel launch
     n_comp = {"sir": 3, "seir": 4}.get(meta["model"], 3 * len(np.atleast_1d(meta["n_population"])))
     bytes_per_unit = 8 * n_comp + 40                                  # 8C+40 B per particle-step
-    achieved = units_per_launch * bytes_per_unit / avg_launch_s / 1e9
+    live_gbs = units_per_launch * bytes_per_unit / avg_launch_s / 1e9
+    # chip level: algorithmic bytes of every particle-step of the timed region over its wall time
+    chip_gbs = filters * N * T * bytes_per_unit / dt / 1e9
     traffic = traffic_raw = None
     valu = None
     rocprof_us = None
     pmc_path = os.path.join(REPO, "profiles", "pmc_step_kernel.json")
+    pmc = {}
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
-            # MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE counts half the bytes of a coalesced read stream, so
-            # `traffic` doubles the read side (FETCH x 2 + WRITE); the raw counter sum is `traffic_raw`
-            per_unit = pmc.get("hbm_bytes_per_particle_step_read_doubled")
-            traffic = per_unit * units_per_launch if per_unit else None
-            raw_unit = pmc.get("hbm_bytes_per_particle_step")
-            traffic_raw = raw_unit * units_per_launch if raw_unit else None
-            # the bound that matters: vector-instruction issue.  SQ_INSTS_VALU per particle-step of
-            # the committed PMC pass (whole-chip sum) x the live rate, against 1024 SIMD-32 x 2.4 GHz / 2 cycles per
-            # wave64 VALU instruction (MI355X_MICROARCH.md); the loop's mix (half VOP3 / 64-bit multiplies at ~4
-            # cycles) caps the reachable fraction near 0.55 of that peak
-            rocprof_us = pmc.get("trace_avg_us")
-            ins = pmc.get("pmc_avg_per_launch", {}).get("SQ_INSTS_VALU")
-            units = pmc.get("particle_steps_per_launch")
-            if ins and units and meta["model"] == "sir":
-                per_ps = ins / units
-                peak = 1024 * 2.4e9 / 2
-                valu = {"achieved": per_ps * value, "peak": peak, "unit": "wave64 VALU instr/s",
-                        "frac": per_ps * value / peak, "instr_per_particle_step": per_ps,
-                        "cycles_per_instr_at_2.4GHz": 1024 * 2.4e9 / (per_ps * value),
-                        # VALU pipe busy per SIMD-cycle, SQ_ACTIVE_INST_VALU / GRBM_GUI_ACTIVE of the PMC pass
-                        # (dispatches serialised there, so each carries its own launch tail)
-                        "pmc_valu_busy_frac": pmc.get("valu_busy_frac")}
         except (OSError, ValueError):
-            traffic = None
+            pmc = {}
+    if pmc.get("config", 2) == args.config and pmc.get("chains_per_gpu", C) == C:
+        # MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE counts half the bytes of a coalesced read stream, so
+        # `traffic` doubles the read side (FETCH x 2 + WRITE); the raw counter sum is `traffic_raw`
+        per_unit = pmc.get("hbm_bytes_per_particle_step_read_doubled")
+        traffic = per_unit * units_per_launch if per_unit else None
+        raw_unit = pmc.get("hbm_bytes_per_particle_step")
+        traffic_raw = raw_unit * units_per_launch if raw_unit else None
+        rocprof_us = pmc.get("trace_avg_us")
+        # the bound: vector-instruction issue.  SQ_INSTS_VALU per particle-step of the committed PMC
+        # pass (whole-chip sum) x the live rate, against 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
+        # instruction (MI355X_MICROARCH.md); the loop's mix (half VOP3 / 64-bit multiplies at ~4 cycles) caps the
+        # reachable fraction near 0.55 of that peak
+        ins = pmc.get("pmc_avg_per_launch", {}).get("SQ_INSTS_VALU")
+        units = pmc.get("particle_steps_per_launch")
+        if ins and units:
+            per_ps = ins / units
+            valu = {"achieved": per_ps * value, "instr_per_particle_step": per_ps,
+                    "cycles_per_instr_at_2.4GHz": VALU_PEAK * 2 / (per_ps * value),
+                    # VALU pipe busy per SIMD-cycle, SQ_ACTIVE_INST_VALU / GRBM_GUI_ACTIVE of the PMC pass
+                    # (dispatches serialised there, so each carries its own launch tail)
+                    "pmc_valu_busy_frac": pmc.get("valu_busy_frac")}
+    hbm_us = rocprof_us or avg_launch_s * 1e6
+    hbm_gbs = units_per_launch * bytes_per_unit / (hbm_us / 1e6) / 1e9
+    hbm = {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
+           "duration_source": "rocprofv3 average kernel duration (profiles/pmc_step_kernel.json)" if rocprof_us
+           else "HIP events (launch to completion)",
+           "frac_hip_event_span": live_gbs / HBM_PEAK_GBS, "chip_level_frac": chip_gbs / HBM_PEAK_GBS,
+           "bytes_per_particle_step": bytes_per_unit, "traffic": traffic, "traffic_raw": traffic_raw}
     # SSA events per second of job time: events per particle-step (counters iteration) x the measured rate
     events_per_s = value * cst["events"] / cst["particle_steps"] if cst["particle_steps"] else None
     lane_use = cst["lane_iterations"] / cst["wave_lane_slots"] if cst["wave_lane_slots"] else None
@@ -273,11 +326,14 @@ def main():
         base = cpu_baseline(Y, meta, N, args.cpu_baseline_seconds)
 
     if rank == 0:
+        # distinct GPUs, not ranks: rehearsals may run several ranks on one device
+        n_gpus = min(world, torch.cuda.device_count()) if world > 1 else 1
         line = {
-            "metric": "particle-steps/sec (N_particles x T_obs x MH-iters) on SIR PMCMC",
+            "metric": f"particle-steps/sec (N_particles x T_obs x MH-iters) on {MODEL_NAMES[meta['model']]} PMCMC",
             "value": value,
             "unit": "particle-steps/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
+            "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt * 1e3 / args.steps,
@@ -290,17 +346,20 @@ def main():
                                    f"pop={meta['n_population']}, {T} obs, {C} independent chains per GPU",
                        "particles": N, "T_obs": T, "chains_per_gpu": C, "population": meta["n_population"],
                        "pipelines": P,
-                       "parallelism": f"chains sharded over {world} GPU(s), RCCL all-gather of draws at end"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_raw": traffic_raw,
-                         "kernel": "pf_step_kernel", "avg_launch_us": avg_launch_s * 1e6,
-                         "bytes_per_particle_step": bytes_per_unit, "particle_steps_per_launch": units_per_launch,
+                       "parallelism": f"chains sharded over {n_gpus} GPU(s) ({world} rank(s)), RCCL all-gather of "
+                                      f"draws at end"},
+            # pf_step_kernel is bound by vector-instruction issue (the SSA event loop), not by HBM: the primary
+            # roofline is VALU issue; the HBM figures the north star asks for are in `hbm`
+            "roofline": {"bound": "valu", "kernel": "pf_step_kernel",
+                         "achieved": valu["achieved"] if valu else None, "peak": VALU_PEAK,
+                         "unit": "wave64 VALU instr/s", "frac": valu["achieved"] / VALU_PEAK if valu else None,
+                         "traffic": traffic, "valu_issue": valu, "hbm": hbm,
+                         "avg_launch_us": avg_launch_s * 1e6, "particle_steps_per_launch": units_per_launch,
                          "concurrent_launches_per_step": streams, "step_wall_us": step_wall_s * 1e6,
                          # the same kernel's average dispatch duration in the committed rocprofv3 trace of this
                          # command (profiles/pmc_step_kernel.json); the HIP-event figure above also counts the time a
                          # launch waits for CUs held by the concurrent chain-group launches
-                         "rocprof_avg_launch_us": rocprof_us,
-                         "valu_issue": valu},
+                         "rocprof_avg_launch_us": rocprof_us},
             "events_per_s": events_per_s,
             "ssa_lane_utilisation": lane_use,
             "resample_fallbacks": st["resample_fallbacks"],
@@ -309,6 +368,7 @@ def main():
             "ssa_exact_particle_frac": cst["ssa_exact_lanes"] / cst["particle_steps"] if cst["particle_steps"] else None,
             "ssa_exact_wave_frac": cst["ssa_exact_waves"] * 64 / cst["particle_steps"] if cst["particle_steps"] else None,
             "gathered_draws_shape": list(gathered.shape),
+            "gathered_rhat": None if rhat is None else [float(x) for x in rhat],
             "cpu_baseline": base,
         }
         if single is not None:
@@ -317,6 +377,9 @@ def main():
             line["single_chain_prefetch"] = prefetch
         if base is not None:
             line["speedup_vs_cpu_baseline"] = value / base["value"]
+            line["speedup_vs_cpu_single_core"] = value / base["single_core"]["value"]
+            if "reference_calibrated" in base:
+                line["speedup_vs_reference_1core_calibrated"] = value / base["reference_calibrated"]["reference_1core_value"]
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

@@ -331,6 +331,15 @@ int oracle_num_threads(void) {
 #endif
 }
 
+/* thread count of the OpenMP loops (bench.py times the port at 1 thread and at the host's allotment) */
+void oracle_set_num_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
 /* scalar weight functions, exported so tests can pin them against scipy (tests/golden/kernels_golden.npz) */
 double oracle_binom_pmf(double k, double n, double p) { return binom_pmf(k, n, p, log(p), log1p(-p)); }
 double oracle_norm_pdf(double y, double x, double probs) { return norm_pdf(y, x, probs); }

@@ -42,6 +42,7 @@ def lib():
         L.oracle_resample.restype = i32
         L.oracle_philox.argtypes = [u32, u32, u32, u32, u64, P]
         L.oracle_num_threads.restype = i32
+        L.oracle_set_num_threads.argtypes = [i32]
         L.oracle_binom_pmf.argtypes = [f64, f64, f64]
         L.oracle_binom_pmf.restype = f64
         L.oracle_norm_pdf.argtypes = [f64, f64, f64]
@@ -143,6 +144,11 @@ def norm_pdf(y, x, probs):
 
 def num_threads():
     return lib().oracle_num_threads()
+
+
+def set_num_threads(n):
+    """OpenMP threads of the filter / SSA loops for the rest of the process."""
+    lib().oracle_set_num_threads(int(n))
 
 
 # ----------------------------------------------------------------------------------- ABC (abc_algo.py:17-109)

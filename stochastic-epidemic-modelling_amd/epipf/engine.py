@@ -215,13 +215,14 @@ _CACHE = {}
 
 
 def get_engine(type_model, groups, n_particles, T, chains=1, device=0):
-    """Cached engine large enough for (T, chains); grows by re-creating when a bigger one is needed."""
+    """Cached engine large enough for (T, chains).  When a bigger one is needed a new context replaces the cached
+    one; the old context is not closed here -- a sampler may still hold it -- but released with its last reference
+    (Engine.__del__).  Callers that share a cached engine re-bind their observations / population before each run
+    (set_observations / set_population are no-ops when nothing changed)."""
     mid = model_id(type_model)
     key = (mid, groups if mid >= _lib.SIR_SUBGROUPS else 1, int(n_particles), int(device))
     eng = _CACHE.get(key)
     if eng is None or eng.t_max < T or eng.max_chains < chains:
-        if eng is not None:
-            eng.close()
         eng = Engine(type_model, groups, n_particles, max(T, eng.t_max if eng else 0),
                      max(chains, eng.max_chains if eng else 0), device)
         _CACHE[key] = eng

@@ -183,6 +183,8 @@ class ChainSampler:
     GPU filter per MH iteration.  `iters` keeps the reference's `n_chains` meaning (MH iterations per
     chain).  Use `initialise()` then `step()` iters-1 times (or `run()`); results via `results()`.
 
+    parameters: the starting theta (pmcmc.py:277), or one per chain as a [chains, d] array; sigma likewise [d, d]
+    or [chains, d, d].
     rngs: per-chain RandomState-like objects (proposals, path picks, acceptance uniforms).
     keys: per-chain Philox keys for the filters; filter indices count from `filter_index_start`."""
 
@@ -193,8 +195,11 @@ class ChainSampler:
         self.keys = np.asarray(keys, dtype=np.uint64)
         nc = self.nc = len(self.rngs)
         mid = self.mid = model_id(type_model)
-        d = self.d = len(parameters)
-        self.parameters = list(parameters)
+        P = np.asarray(parameters, dtype=np.float64)
+        d = self.d = P.shape[-1]
+        # per-chain starting points (a [chains, d] array, e.g. warm starts, chains_io.warm_start) or one for all
+        self.params = [(P[c] if P.ndim == 2 else P).tolist() for c in range(nc)]
+        self.parameters = self.params[0] if nc else P.tolist()
         self.probs = probs
         self.h = h
         self.adaptive = adaptive
@@ -215,13 +220,14 @@ class ChainSampler:
             if (eng.model, eng.G, eng.N) != (mid, G, self.N) or eng.t_max < T or eng.max_chains < max(nc, engine_chains):
                 raise ValueError("engine does not match the model / particles / T / chains of this sampler")
         self.eng = eng
-        eng.set_observations(Y)
-        eng.set_population(npop, mus)
+        self._Y, self._npop, self._mus = Y, npop, mus
+        self._bind()
         self.thetas = np.zeros((nc, self.iters, d))
         self.likelihoods = np.zeros((nc, self.iters))
         self.loglik = np.zeros((nc, self.iters))
         self.trajs = np.zeros((nc, T, self.iters, Cc))
-        self.std = [np.eye(d) if sigma is None else np.asarray(sigma, dtype=np.float64) for _ in range(nc)]
+        S = None if sigma is None else np.asarray(sigma, dtype=np.float64)
+        self.std = [np.eye(d) if S is None else (S[c] if S.ndim == 3 else S).copy() for c in range(nc)]
         self._fac = [None] * nc                                  # multivariate_normal factor of h * std[c]
         self.fnext = [int(filter_index_start)] * nc
         self.filters_run = [0] * nc
@@ -229,6 +235,13 @@ class ChainSampler:
         self.dth = d - (1 if probs is None else 0)
         self.i = 0
         self.last_active = 0
+
+    def _bind(self):
+        """(Re)load this sampler's observations and population into its engine before a run: a cached engine is
+        shared with every other sampler / particle_filter call of the same model, N and device (no-op when
+        unchanged, engine.set_observations / set_population compare first)."""
+        self.eng.set_observations(self._Y)
+        self.eng.set_population(self._npop, self._mus)
 
     def _propose(self, c, mean):
         """rngs[c].multivariate_normal(mean, h * std[c]) (pmcmc.py:277, :330) with the SVD factor cached per chain."""
@@ -261,6 +274,7 @@ class ChainSampler:
             fidx[c] = self.fnext[c]
             self.fnext[c] += 1
             self.filters_run[c] += 1
+        self._bind()
         lz, st = self.eng.run(th_all, pr_all, self.keys, fidx, observations=self.observations, active=act,
                               resample=self.resample)
         self.last_active = len(props)
@@ -284,7 +298,7 @@ class ChainSampler:
         while pending:
             props = {}
             for c in pending:
-                prop = self._propose(c, np.array(self.parameters))
+                prop = self._propose(c, np.array(self.params[c]))
                 if sum(prop < 0) > 0:
                     continue
                 props[c] = prop
@@ -330,7 +344,7 @@ class ChainSampler:
                 theta_new = np.append(th, p2) if self.probs is None else props[c]
                 if self.mh_ratio == "reference":
                     prob = _reference_ratio(np.exp(lz[c, -1]), self.likelihoods[c, i - 1], theta_new,
-                                            self.thetas[c, i - 1], self.parameters, self.h * self.std[c])
+                                            self.thetas[c, i - 1], self.params[c], self.h * self.std[c])
                 else:
                     prob = _log_ratio(lz[c, -1], self.loglik[c, i - 1])
                 if self.rngs[c].random_sample() < prob:            # == uniform(): 0 + 1*U, 7x cheaper

@@ -187,7 +187,7 @@ class PrefetchSampler(ChainSampler):
         z_old, lz_old, _ = cur
         z_new = np.exp(lzr[-1])
         if self.mh_ratio == "reference":
-            prob = _reference_ratio(z_new, z_old, x.theta_new, x.theta, self.parameters, self.h * self._std_for(x))
+            prob = _reference_ratio(z_new, z_old, x.theta_new, x.theta, self.params[x.chain], self.h * self._std_for(x))
         else:
             prob = _log_ratio(lzr[-1], lz_old)
         return x.kids[0] if x.u < prob else x.kids[1]
@@ -235,6 +235,7 @@ class PrefetchSampler(ChainSampler):
             th_all[s], pr_all[s] = x.stripped
             keys[s] = self.keys[x.chain]
             fidx[s] = x.fnext
+        self._bind()
         lz, st = self.eng.run(th_all, pr_all, keys, fidx, observations=self.observations, resample=self.resample)
         chosen = np.array([x.chosen for x in nodes], dtype=np.int32)
         tr = self.eng.path_sample(chosen) if np.any(st == _lib.STATUS_OK) else None
@@ -316,10 +317,21 @@ class PrefetchSampler(ChainSampler):
     def run(self, progress=False, on_iteration=None):
         if self.roots is None:
             self.initialise()
+        bar = None
+        if progress:                                            # the reference's chain bar, pmcmc.py:320-406
+            from tqdm import tqdm
+            bar = tqdm(total=self.iters - 1, desc="Chains", position=1)
         while self.i < self.iters:
             before = self.i
             self.advance()
+            if bar is not None and self.i > before:
+                i = self.i - 1
+                bar.update(self.i - before)
+                bar.set_postfix_str(f"accepted_theta: {self.thetas[0, i]}, "
+                                    f"acceptance_ratio: {100 * self.acceptances[0] / (i + 1)}%")
             if on_iteration is not None:
                 for k in range(before, self.i):
                     on_iteration(k, None)
+        if bar is not None:
+            bar.close()
         return self.results()

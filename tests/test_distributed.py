@@ -12,6 +12,7 @@ import torch.multiprocessing as mp
 
 from epipf import distributed as D
 from epipf import pmcmc as pm
+from epipf.chains_io import gelman_rubin, save_run, warm_start
 from oracle_engine import fake_get_engine
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -28,7 +29,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, Y, total, paths, q, prefetch=0):
+def _worker(rank, world, port, Y, total, paths, q, prefetch=0, extra=None):
     for p in paths:
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -40,8 +41,8 @@ def _worker(rank, world, port, Y, total, paths, q, prefetch=0):
     pmw.get_engine = fge
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res, ids, th, ll = Dw.sharded_pmcmc(Y, "sir", [2.0, 1.0], 0.01, total, seed=9, prefetch=prefetch, **KW)
-        q.put((rank, ids, th, ll))
+        run = Dw.sharded_pmcmc(Y, "sir", [2.0, 1.0], 0.01, total, seed=9, prefetch=prefetch, **{**KW, **(extra or {})})
+        q.put((rank, run.ids, run.thetas, run.log_likelihoods, run.rhat))
     finally:
         dist.barrier()
         dist.destroy_process_group()
@@ -77,23 +78,66 @@ def test_gloo_world2_gather_equals_single_process(monkeypatch, datasets_golden, 
     the gathered draws equal a one-process lockstep run of every chain."""
     Y = datasets_golden["cfg1_binom"][:6]
     monkeypatch.setattr(pm, "get_engine", fake_get_engine)
-    _, ids, th1, ll1 = D.sharded_pmcmc(Y, "sir", [2.0, 1.0], 0.01, total, seed=9, **KW)
-    assert ids == list(range(total))
+    one = D.sharded_pmcmc(Y, "sir", [2.0, 1.0], 0.01, total, seed=9, **KW)
+    assert one.ids == list(range(total))
+    out = _run_world2(Y, total, prefetch)
+    assert out[0][0] + out[1][0] == list(range(total))
+    for rank in (0, 1):
+        np.testing.assert_array_equal(out[rank][1], one.thetas)   # every rank holds all chains, in global order
+        np.testing.assert_array_equal(out[rank][2], one.log_likelihoods)
+        np.testing.assert_array_equal(out[rank][3], one.rhat)     # R-hat of the gathered chains, on every rank
+    np.testing.assert_array_equal(one.rhat, gelman_rubin([r.thetas for r in one.results]))
+
+
+def _run_world2(Y, total, prefetch=0, extra=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     paths = [HERE] + [p for p in sys.path if "stochastic-epidemic" in p or p.endswith("oracle")]
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, Y, total, paths, q, prefetch)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, Y, total, paths, q, prefetch, extra)) for r in range(2)]
     for p in procs:
         p.start()
     out = {}
     for _ in range(2):
-        rank, ids_r, th, ll = q.get(timeout=240)
-        out[rank] = (ids_r, th, ll)
+        rank, ids_r, th, ll, rhat = q.get(timeout=240)
+        out[rank] = (ids_r, th, ll, rhat)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert out[0][0] + out[1][0] == list(range(total))
+    return out
+
+
+def test_gloo_world2_save_and_resume(monkeypatch, datasets_golden, tmp_path):
+    """Each rank writes its chains in the reference's CSV layout (one directory per global chain id); a second
+    sharded run resumes every chain from the warm start of its own saved run.  Both equal a one-process run, and
+    the files are byte-identical to np.savetxt of the one-process results (tests/experiments/pobs/prob_.05.py:57-61)."""
+    Y = datasets_golden["cfg1_binom"][:6]
+    monkeypatch.setattr(pm, "get_engine", fake_get_engine)
+    total = 3
+    kw = dict(KW, n_chains=8)
+    one = D.sharded_pmcmc(Y, "sir", [2.0, 1.0], 0.01, total, seed=9, save_dir=str(tmp_path / "one"), **kw)
+    for g, r in enumerate(one.results):
+        ref = tmp_path / "ref"
+        save_run(str(ref), r.thetas, r.likelihoods, r.sampled_trajs)
+        for f in sorted(os.listdir(ref)):
+            assert (ref / f).read_bytes() == open(os.path.join(D.chain_dir(str(tmp_path / "one"), g), f), "rb").read()
+    two = str(tmp_path / "two")
+    _run_world2(Y, total, extra=dict(save_dir=two, n_chains=8))
+    for g in range(total):
+        for f in os.listdir(D.chain_dir(str(tmp_path / "one"), g)):
+            assert open(os.path.join(D.chain_dir(two, g), f), "rb").read() == \
+                open(os.path.join(D.chain_dir(str(tmp_path / "one"), g), f), "rb").read()
+    # resume: start at each chain's last draw with its own covariance (burn-in 2, thin 2)
+    res_kw = dict(resume_dir=two, resume_burn_in=2, resume_thin=2)
+    one_r = D.sharded_pmcmc(Y, "sir", [2.0, 1.0], 0.01, total, seed=11, **res_kw, **kw)
+    for g, r in enumerate(one_r.results):
+        th0, sig = warm_start(one.results[g].thetas, 2, 2)
+        single = pm.particle_mcmc_chains(Y, "sir", th0, 0.01, rngs=[np.random.RandomState(11 + g)],
+                                         keys=[pm.chain_key(11, g)], **{**kw, "sigma": sig})[0]
+        np.testing.assert_array_equal(r.thetas, single.thetas)
+    out = _run_world2(Y, total, extra=dict(n_chains=8, **res_kw))
+    # the worker's seed is 9: compare with a one-process resume at seed 9
+    one_r9 = D.sharded_pmcmc(Y, "sir", [2.0, 1.0], 0.01, total, seed=9, **res_kw, **kw)
     for rank in (0, 1):
-        np.testing.assert_array_equal(out[rank][1], th1)   # every rank holds all chains, in global order
-        np.testing.assert_array_equal(out[rank][2], ll1)
+        np.testing.assert_array_equal(out[rank][1], one_r9.thetas)
+        np.testing.assert_array_equal(out[rank][3], one_r9.rhat)

@@ -548,3 +548,42 @@ def test_filter_short_horizons_and_extinct_starts_vs_oracle(datasets_golden, mod
     np.testing.assert_array_equal(hid[0], o["hidden"])
     np.testing.assert_array_equal(anc[0], o["ancestry"])
     np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("cfg,chains,T", [(3, 2, None), (4, 2, None), (5, 2, None)])
+def test_full_size_baseline_configs_vs_oracle(cfg, chains, T):
+    """BASELINE configs 3 (SEIR, normal observations, N = 10^4, T = 200), 4 (SIR under-reported, N = 5*10^4, all 15
+    rows: segmented block prefix) and 5 (2-group SIR, N = 10^4) at their full bench size, on the bench's own
+    dataset and starting theta plus a perturbed theta (one batched launch, one chain each): states and ancestors
+    bit-exact vs the oracle (pmcmc.py:123-233 restated), log-likelihoods within 1e-9 absolute."""
+    from epipf import datasets
+    from epipf.engine import Engine, model_id, theta_vector
+    Y, meta = datasets.benchmark_dataset(cfg)
+    if T:
+        Y = Y[:T]
+    N = meta["N"]
+    mid = model_id(meta["model"])
+    base = np.asarray(meta["theta"], dtype=np.float64)
+    thetas = np.stack([base * (1.0 + 0.07 * c * (-1) ** np.arange(base.size)) for c in range(chains)])
+    if mid >= 2:
+        G = int(round(np.sqrt(base.size - 1)))
+        ref_th = [(t[:G * G].reshape(G, G), t[-1]) for t in thetas]
+    else:
+        G = 1
+        ref_th = [tuple(t) for t in thetas]
+    eng = Engine(meta["model"], G, N, Y.shape[0], chains)
+    eng.set_observations(Y)
+    eng.set_population(meta["n_population"], meta["mu"])
+    obs = bool(meta.get("observations", False))
+    keys = [9000 + 17 * c for c in range(chains)]
+    lz, st = eng.run(np.stack([theta_vector(mid, t)[0] for t in ref_th]), [meta["probs"]] * chains, keys,
+                     [5 + c for c in range(chains)], observations=obs)
+    hid, anc = eng.history(chains)
+    eng.close()
+    for c in range(chains):
+        o = oracle.particle_filter(Y, meta["model"], ref_th[c], obs, meta["probs"], N, meta["n_population"],
+                                   meta["mu"], key=keys[c], filter_index=5 + c)
+        assert int(st[c]) == o["status"] == 0, (c, st[c], o["status"])
+        np.testing.assert_array_equal(hid[c], o["hidden"])
+        np.testing.assert_array_equal(anc[c], o["ancestry"])
+        np.testing.assert_allclose(lz[c], o["log_zetas"], rtol=1e-12, atol=1e-9)
