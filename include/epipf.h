@@ -13,6 +13,7 @@
  *                        (the uniform pick np.random.randint(0, N) stays on the host RNG: `chosen`)
  *   epipf_simulate       gillespie_algo.py:10-75 / 78-146 / 148-233  sir_simulate / seir_simulate /
  *                        sir_subgroups_simulate(..., last_values_only=True), batched over states
+ *   epipf_simulate_path  the same functions with last_values_only=False (event times + states)
  *   epipf_resample       pmcmc.py:185-190  normalise + np.random.choice(range(N), N, p=w/sum(w)) with
  *                        caller-supplied uniforms (bit-exact to numpy's legacy choice)
  *   epipf_abc            abc_algo.py:17-109  abc_algo(observed_data, no_of_samples, threshold, priors)
@@ -38,7 +39,7 @@
 extern "C" {
 #endif
 
-#define EPIPF_ABI_VERSION 3
+#define EPIPF_ABI_VERSION 4
 
 /* return codes */
 #define EPIPF_OK 0
@@ -127,6 +128,16 @@ int epipf_simulate(epipf_ctx* ctx, int n, const int32_t* states_in, const double
                    double max_time, uint64_t key, uint32_t filter_index, uint32_t step, int32_t* states_out,
                    int64_t* events_out);
 
+/* Batched full-path SSA (gillespie_algo.py *_simulate with last_values_only=False, :68-75 / :139-146 /
+ * :218-233): the same draws and final states as epipf_simulate, plus every event's time and the state after it.
+ * Trajectory j keeps its first max_events events: times_out [n*max_events] (row j: its event times, ascending),
+ * states_out [n*max_events*C]; n_events_out [n] is its full event count (> max_events: the rows hold the first
+ * max_events only, call again with a larger buffer); final_out [n*C] (or NULL) its last state.  The event times
+ * are the reference's clock bit for bit.  The initial state (time 0.0) is the caller's input. */
+int epipf_simulate_path(epipf_ctx* ctx, int n, const int32_t* states_in, const double* theta, int d,
+                        double max_time, uint64_t key, uint32_t filter_index, uint32_t step, int max_events,
+                        double* times_out, int32_t* states_out, int32_t* n_events_out, int32_t* final_out);
+
 /* Standalone resampler: out[j] = numpy legacy choice(range(n), n, p=w/sum(w)) given uniforms u[j].
  * Returns EPIPF_STATUS_DEGENERATE (as a positive value) where numpy raises ValueError. */
 int epipf_resample(epipf_ctx* ctx, int n, const double* w, const double* u, int32_t* out,
@@ -151,6 +162,11 @@ int epipf_abc(epipf_ctx* ctx, const double* Y, int T, int no_of_samples, double 
 /* Trials [t0, t0+n): theta_out [n*2]; rows_out [n*T*3] int32 (S, I, R per day) or NULL; dist_out [n] or NULL. */
 int epipf_abc_trials(epipf_ctx* ctx, const double* Y, int T, const double* priors, uint64_t key, uint32_t run_index,
                      uint32_t t0, int n, double* theta_out, int32_t* rows_out, double* dist_out, int64_t* events_out);
+
+/* The device's restatement of glibc's log (the reference's math.log / numpy legacy exponential),
+ * evaluated on the host CPU with the same code and table: out[i] = log(x[i]) bit for bit for normal x[i] > 0.
+ * For tests of that restatement; no GPU involved. */
+int epipf_glibc_log(int64_t n, const double* x, double* out);
 
 /* Profiling levels: OFF; TIMING = HIP events around the init / step kernels (step_ms, init_ms), no effect on
  * the kernels; COUNTERS = TIMING + device counters of SSA events and lane use (a few atomics per wave). */

@@ -65,10 +65,21 @@ typedef struct {
     double theta[MAXCH + 1];  /* SIR: beta,gamma  SEIR: beta,alpha,gamma  groups: beta[G][G] row-major, gamma */
 } model_t;
 
+/* Full-path recorder (gillespie_algo.py last_values_only=False: conditions["time"] and the compartments after
+ * every event, :68-70): the first `cap` events' times and states. */
+typedef struct { long cap; double* t; int32_t* x; int C; } path_t;
+
+static void record(path_t* pth, long nev, double t, const double* st) {
+    if (!pth || nev > pth->cap) return;
+    pth->t[nev - 1] = t;
+    for (int c = 0; c < pth->C; ++c) pth->x[(size_t)(nev - 1) * pth->C + c] = (int32_t)st[c];
+}
+
 /* Gillespie direct method over [0, max_time], gillespie_algo.py.  State in x[] (ints held as doubles,
- * exactly as the reference holds them in float64).  Returns the number of accepted events. */
-static long ssa(const model_t* m, double* x, double max_time, uint64_t key, uint32_t f, uint32_t ptag,
-                uint32_t j) {
+ * exactly as the reference holds them in float64).  Returns the number of accepted events; `pth` (or NULL)
+ * records the path. */
+static long ssa_path(const model_t* m, double* x, double max_time, uint64_t key, uint32_t f, uint32_t ptag,
+                     uint32_t j, path_t* pth) {
     uint32_t r[4];
     double t = 0.0;
     uint32_t k = 0;
@@ -90,6 +101,7 @@ static long ssa(const model_t* m, double* x, double max_time, uint64_t key, uint
             t = t + tau;                                                /* :68 */
             if (ch == 0) { S -= 1.0; I += 1.0; } else { I -= 1.0; R += 1.0; }   /* :43-46, :69-70 */
             ++nev;
+            if (pth) { const double st[3] = {S, I, R}; record(pth, nev, t, st); }
         }
         x[0] = S; x[1] = I; x[2] = R;
     } else if (m->model == M_SEIR) {
@@ -111,6 +123,7 @@ static long ssa(const model_t* m, double* x, double max_time, uint64_t key, uint
             else if (ch == 1) { E -= 1.0; I += 1.0; }
             else { I -= 1.0; R += 1.0; }                                /* :113-117 */
             ++nev;
+            if (pth) { const double st[4] = {S, E, I, R}; record(pth, nev, t, st); }
         }
         x[0] = S; x[1] = E; x[2] = I; x[3] = R;
     } else {
@@ -145,12 +158,22 @@ static long ssa(const model_t* m, double* x, double max_time, uint64_t key, uint
             if (w < G) { S[w] -= 1.0; I[w] += 1.0; }                    /* s_{g}_{g2}: S_g2 -> I_g2, :183 */
             else { I[g] -= 1.0; R[g] += 1.0; }                          /* i_{g}: I_g -> R_g, :185 */
             ++nev;
+            if (pth) {
+                double st[MAXC];
+                for (int q = 0; q < G; ++q) { st[3 * q] = S[q]; st[3 * q + 1] = I[q]; st[3 * q + 2] = R[q]; }
+                record(pth, nev, t, st);
+            }
             infected = 0.0;
             for (int q = 0; q < G; ++q) infected = infected + I[q];     /* :222 */
         }
         for (int g = 0; g < G; ++g) { x[3 * g] = S[g]; x[3 * g + 1] = I[g]; x[3 * g + 2] = R[g]; }
     }
     return nev;
+}
+
+static long ssa(const model_t* m, double* x, double max_time, uint64_t key, uint32_t f, uint32_t ptag,
+                uint32_t j) {
+    return ssa_path(m, x, max_time, key, f, ptag, j, NULL);
 }
 
 static int load_model(model_t* m, int model, int G, const double* theta, int d) {
@@ -180,6 +203,26 @@ int oracle_simulate(int model, int G, int n, const int32_t* states_in, const dou
         for (int c = 0; c < m.C; ++c) states_out[(size_t)j * m.C + c] = (int32_t)x[c];
     }
     if (events_out) *events_out = total;
+    return 0;
+}
+
+/* Batched full-path SSA (gillespie_algo.py *_simulate(..., last_values_only=False)): trajectory j's first `cap`
+ * event times times_out[j*cap + e] and states states_out[(j*cap + e)*C + c]; nev_out[j] its event count (may
+ * exceed cap); final_out[j*C + c] its last state. */
+int oracle_simulate_path(int model, int G, int n, const int32_t* states_in, const double* theta, int d,
+                         double max_time, uint64_t key, uint32_t f, uint32_t step, long cap, double* times_out,
+                         int32_t* states_out, int32_t* nev_out, int32_t* final_out) {
+    model_t m;
+    if (load_model(&m, model, G, theta, d) || cap < 0) return -1;
+    const uint32_t ptag = (step & 0xFFFFFFu) | ((uint32_t)DOM_SSA << 24);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int j = 0; j < n; ++j) {
+        double x[MAXC];
+        for (int c = 0; c < m.C; ++c) x[c] = (double)states_in[(size_t)j * m.C + c];
+        path_t pth = {cap, times_out + (size_t)j * cap, states_out + (size_t)j * cap * m.C, m.C};
+        nev_out[j] = (int32_t)ssa_path(&m, x, max_time, key, f, ptag, (uint32_t)j, &pth);
+        for (int c = 0; c < m.C; ++c) final_out[(size_t)j * m.C + c] = (int32_t)x[c];
+    }
     return 0;
 }
 
@@ -338,6 +381,11 @@ void oracle_set_num_threads(int n) {
 #else
     (void)n;
 #endif
+}
+
+/* glibc's log over an array (what the reference's math.log returns), to pin the device's restatement */
+void oracle_log_batch(long n, const double* x, double* out) {
+    for (long i = 0; i < n; ++i) out[i] = log(x[i]);
 }
 
 /* scalar weight functions, exported so tests can pin them against scipy (tests/golden/kernels_golden.npz) */

@@ -38,11 +38,14 @@ def lib():
         L.oracle_particle_filter.restype = i32
         L.oracle_simulate.argtypes = [i32, i32, i32, P, P, i32, f64, u64, u32, u32, P, P]
         L.oracle_simulate.restype = i32
+        L.oracle_simulate_path.argtypes = [i32, i32, i32, P, P, i32, f64, u64, u32, u32, ctypes.c_long, P, P, P, P]
+        L.oracle_simulate_path.restype = i32
         L.oracle_resample.argtypes = [i32, P, P, P]
         L.oracle_resample.restype = i32
         L.oracle_philox.argtypes = [u32, u32, u32, u32, u64, P]
         L.oracle_num_threads.restype = i32
         L.oracle_set_num_threads.argtypes = [i32]
+        L.oracle_log_batch.argtypes = [ctypes.c_long, P, P]
         L.oracle_binom_pmf.argtypes = [f64, f64, f64]
         L.oracle_binom_pmf.restype = f64
         L.oracle_norm_pdf.argtypes = [f64, f64, f64]
@@ -116,6 +119,34 @@ def simulate(type_model, states, theta, max_time=1.0, key=0, filter_index=0, ste
     return out, int(ev[0])
 
 
+def simulate_path(type_model, states, theta, max_time=1.0, key=0, filter_index=0, step=0, cap=None):
+    """Batched full-path SSA (gillespie_algo.*_simulate(..., last_values_only=False)) from int states [n, C].
+    Returns (times [n, cap], states [n, cap, C], n_events [n], final [n, C]); cap defaults to the longest path."""
+    mid = model_id(type_model)
+    th, G = _theta_vector(mid, theta)
+    states = np.ascontiguousarray(np.asarray(states, dtype=np.int32))
+    n, C = states.shape
+    if cap is None:
+        _, nev, _ = _path_once(mid, G, states, th, max_time, key, filter_index, step, 0)
+        cap = int(nev.max()) if n else 0
+    return _path_once(mid, G, states, th, max_time, key, filter_index, step, cap, full=True)
+
+
+def _path_once(mid, G, states, th, max_time, key, f, step, cap, full=False):
+    n, C = states.shape
+    t = np.zeros((n, max(cap, 1)))
+    x = np.zeros((n, max(cap, 1), C), dtype=np.int32)
+    nev = np.zeros(n, dtype=np.int32)
+    fin = np.zeros((n, C), dtype=np.int32)
+    st = lib().oracle_simulate_path(mid, G, n, _p(states), _p(th), len(th), float(max_time), int(key) & (2**64 - 1),
+                                    int(f) & 0xFFFFFFFF, int(step), int(cap), _p(t), _p(x), _p(nev), _p(fin))
+    if st < 0:
+        raise ValueError("oracle_simulate_path: bad arguments")
+    if full:
+        return t[:, :cap], x[:, :cap], nev, fin
+    return t, nev, fin
+
+
 def resample(w, u):
     """numpy legacy choice(range(N), N, p=w/sum(w)) with the given uniforms; None where numpy raises."""
     w = np.ascontiguousarray(np.asarray(w, dtype=np.float64))
@@ -144,6 +175,14 @@ def norm_pdf(y, x, probs):
 
 def num_threads():
     return lib().oracle_num_threads()
+
+
+def log_batch(x):
+    """glibc log (libm, the reference's math.log) of every element."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.empty_like(x)
+    lib().oracle_log_batch(x.size, _p(x), _p(out))
+    return out
 
 
 def set_num_threads(n):

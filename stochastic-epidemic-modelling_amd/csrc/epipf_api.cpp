@@ -222,7 +222,9 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
         free_ctx(c);
         return fail(EPIPF_EHIP, "hipEventCreate failed");
     }
-    if (launch_log_table(c->logtab, c->stream) != hipSuccess ||
+    LogTab lt[kLogTabEntries];
+    glibc_log_table(lt);
+    if (hipMemcpy(c->logtab, lt, sizeof lt, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
         free_ctx(c);
@@ -487,6 +489,75 @@ int epipf_simulate(epipf_ctx* c, int n, const int32_t* states_in, const double* 
     HIP_TRY(hipMemcpyAsync(&ev, dev_events, sizeof ev, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (events_out) *events_out = (int64_t)ev;
+    return EPIPF_OK;
+}
+
+int epipf_simulate_path(epipf_ctx* c, int n, const int32_t* states_in, const double* theta, int d, double max_time,
+                        uint64_t key, uint32_t filter_index, uint32_t step, int max_events, double* times_out,
+                        int32_t* states_out, int32_t* n_events_out, int32_t* final_out) {
+    if (!c || !states_in || !theta || !n_events_out) return fail(EPIPF_EINVAL, "NULL argument");
+    if (n < 0 || max_events < 0) return fail(EPIPF_EINVAL, "n and max_events must be >= 0");
+    if (max_events > 0 && (!times_out || !states_out)) return fail(EPIPF_EINVAL, "NULL path output");
+    if (d != theta_dim(c->model, c->G)) return fail(EPIPF_EINVAL, "theta needs %d entries", theta_dim(c->model, c->G));
+    if (!(max_time >= 0.0)) return fail(EPIPF_EINVAL, "max_time must be >= 0");
+    for (int i = 0; i < d; ++i)
+        if (!(theta[i] >= 0.0 && theta[i] < INFINITY)) return fail(EPIPF_EINVAL, "theta[%d] must be finite and >= 0", i);
+    for (size_t i = 0; i < (size_t)n * c->C; ++i)
+        if (states_in[i] < 0) return fail(EPIPF_EINVAL, "states must be non-negative");
+    if (n == 0) return EPIPF_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    const int C = c->C;
+    const size_t cap = (size_t)max_events;
+    const size_t sb = align256((size_t)n * C * sizeof(int32_t));
+    const size_t tb = align256(cap * n * sizeof(double)), xb = align256(cap * n * C * sizeof(int32_t));
+    const size_t nb = align256((size_t)n * sizeof(int32_t));
+    const size_t need = align256(sizeof(ChainParam)) + 2 * sb + tb + xb + nb;
+    if (ensure_scratch(c, need)) return EPIPF_ENOMEM;
+    char* base = (char*)c->scratch;
+    ChainParam* dcp = (ChainParam*)base;
+    int32_t* din = (int32_t*)(base + align256(sizeof(ChainParam)));
+    int32_t* dfin = (int32_t*)((char*)din + sb);
+    double* dt = (double*)((char*)dfin + sb);
+    int32_t* dx = (int32_t*)((char*)dt + tb);
+    int32_t* dnev = (int32_t*)((char*)dx + xb);
+    ChainParam q;
+    memset(&q, 0, sizeof q);
+    for (int i = 0; i < d; ++i) { q.theta[i] = theta[i]; q.thetaf[i] = (float)theta[i]; }
+    q.k0 = (uint32_t)key; q.k1 = (uint32_t)(key >> 32); q.f = filter_index;
+    HIP_TRY(hipMemcpyAsync(dcp, &q, sizeof q, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(din, states_in, sizeof(int32_t) * (size_t)n * C, hipMemcpyHostToDevice, c->stream));
+    SimPathArgs a{};
+    a.logtab = c->logtab; a.n = n; a.cap = max_events; a.step = step; a.tmax = max_time; a.cp = dcp; a.in = din;
+    a.times = dt; a.states = dx; a.nev = dnev; a.final_state = dfin;
+    hipError_t le = launch_simulate_path(a, c->model, c->G, c->stream);
+    if (le != hipSuccess) return fail(EPIPF_EHIP, "simulate_path launch failed: %s", hipGetErrorString(le));
+    HIP_TRY(hipMemcpyAsync(n_events_out, dnev, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    if (final_out)
+        HIP_TRY(hipMemcpyAsync(final_out, dfin, sizeof(int32_t) * (size_t)n * C, hipMemcpyDeviceToHost, c->stream));
+    std::vector<double> ht;
+    std::vector<int32_t> hx;
+    if (cap > 0) {
+        ht.resize(cap * n);
+        hx.resize(cap * n * C);
+        HIP_TRY(hipMemcpyAsync(ht.data(), dt, sizeof(double) * cap * n, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(hx.data(), dx, sizeof(int32_t) * cap * n * C, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int j = 0; j < n; ++j) {                       // event-major device rows -> one row per trajectory
+        const size_t m = std::min<size_t>(cap, (size_t)std::max(n_events_out[j], 0));
+        for (size_t e = 0; e < m; ++e) {
+            times_out[(size_t)j * cap + e] = ht[e * n + j];
+            for (int k = 0; k < C; ++k) states_out[((size_t)j * cap + e) * C + k] = hx[(e * C + k) * n + j];
+        }
+    }
+    return EPIPF_OK;
+}
+
+int epipf_glibc_log(int64_t n, const double* x, double* out) {
+    if (n < 0 || (n > 0 && (!x || !out))) return fail(EPIPF_EINVAL, "NULL argument");
+    LogTab lt[kLogTabEntries];
+    glibc_log_table(lt);
+    for (int64_t i = 0; i < n; ++i) out[i] = glibc_log(x[i], lt);
     return EPIPF_OK;
 }
 

@@ -83,82 +83,68 @@ struct ChainParam {
 };
 constexpr uint32_t kChainFastSsa = 1u;   // (all models)
 
-// ------------------------------------------------------------------------------- f64 log, table driven
-// log(x) for normal x > 0, within 1 ulp of glibc's correctly rounded log (exact near x = 1).  x = 2^k z with
-// z in [0.6875, 1.375) (glibc's OFF reduction); z is centred on one of 128 table points c_i
-// (LogTab: {1/c_i, log c_i}), r = z/c_i - 1 (|r| < 2^-8) and log1p(r) is a degree-7 polynomial.  Inputs within
-// 2^-8 of 1 bypass the table (r = x - 1 exactly).  ~20 instructions against ~45 for the library log.
+// ------------------------------------------------------------------------------- reference-exact log
+// glibc 2.35 log(x), the function behind the reference's draws (numpy legacy exponential = scale * -log(1 - U),
+// gillespie_algo.py:62; the keyed-stream shim's math.log): sysdeps/ieee754/dbl-64/e_log.c as the x86_64 libm
+// runs it on an FMA CPU (__log_fma, e_log.c compiled with -mfma -mavx2).  Same table (__log_data, copied from
+// this machine's libm at build time by gen_glibc_log.py), same operations, same fused multiply-adds -- read off
+// that function's machine code -- so every result is the library's bit for bit (tests/test_glibc_log.py compares
+// >= 10^8 inputs with math.log).  Defined for normal x > 0 (the SSA calls it on 1 - U >= 2^-53).
+// Host-callable too: epipf_glibc_log (epipf_api.cpp) runs this code on the CPU for that test.
+#include "glibc_log_data.inc"
+
 struct LogTab { double invc, logc; };
 constexpr int kLogTabEntries = 128;
-constexpr uint64_t kLogOff = 0x3FE6000000000000ull;   // 0.6875
 
-// one entry per thread (i < 128); the bin holding 1.0 gets exactly {1, 0}
-__device__ __forceinline__ void log_table_entry(LogTab* tab, int i) {
-    if (i < kLogTabEntries) {
-        const double c = __longlong_as_double((long long)(kLogOff + ((uint64_t)(2 * i + 1) << 44)));
-        const double ic = 1.0 / c;
-        const bool one = i == (int)(((0x3FF0000000000000ull - kLogOff) >> 45) & 127);
-        tab[i].invc = one ? 1.0 : ic;
-        tab[i].logc = one ? 0.0 : -log(ic);
+__host__ __device__ inline double glibc_log(double x, const LogTab* __restrict__ tab) {
+    const uint64_t ix = __builtin_bit_cast(uint64_t, x);
+    constexpr uint64_t LO = 0x3FEE000000000000ull;                    // asuint64(1 - 0x1p-4)
+    constexpr uint64_t HI = 0x3FF1090000000000ull;                    // asuint64(1 + 0x1.09p-4)
+    if (ix - LO < HI - LO) {                                          // inputs close to 1: poly1 (B), no table
+        if (ix == 0x3FF0000000000000ull) return 0.0;
+        const double r = x - 1.0;
+        const double r2 = r * r, r3 = r * r2;
+        double q1 = fma(r, kGlibcLogB[2], kGlibcLogB[1]);
+        double q4 = fma(r, kGlibcLogB[5], kGlibcLogB[4]);
+        double q7 = fma(r, kGlibcLogB[8], kGlibcLogB[7]);
+        q1 = fma(r2, kGlibcLogB[3], q1);
+        q4 = fma(r2, kGlibcLogB[6], q4);
+        q7 = fma(r2, kGlibcLogB[9], q7);
+        q7 = fma(r3, kGlibcLogB[10], q7);
+        q4 = fma(q7, r3, q4);
+        const double poly = fma(q4, r3, q1);                          // y = r3 (B1 + r B2 + r2 B3 + r3 (...))
+        const double rhi = fma(-0x1.0p27, r, fma(r, 0x1.0p27, r));    // w = r 2^27; rhi = r + w - w
+        const double rlo = r - rhi;
+        const double rr = rhi * rhi;
+        const double hi = fma(rr, kGlibcLogB[0], r);                  // w = rhi rhi B0; hi = r + w
+        double lo = fma(rr, kGlibcLogB[0], r - hi);                   // lo = r - hi + w
+        lo = fma(kGlibcLogB[0] * rlo, r + rhi, lo);                   // lo += B0 rlo (rhi + r)
+        return hi + fma(poly, r3, lo);                                // y += lo; y += hi
     }
-}
-
-// Index, exponent and reduced argument are formed on the high 32-bit word (kLogOff's low word is zero, so
-// ix - kLogOff never borrows); inputs within 2^-8 of 1 select the exact {1, 0} bin with k = 0, z = x, so
-// r = x - 1 exactly -- no branch.
-// P(r) = 1/7 r^5 - 1/6 r^4 + 1/5 r^3 - 1/4 r^2 + 1/3 r - 1/2 by Horner, as five dependent three-operand
-// v_fma_f64 with the constants in SGPR pairs, in one asm block: hipcc otherwise copies each constant into
-// the destination of a two-address v_fmac_f64 (one 64-bit move per step), and separate asm statements get
-// an s_nop between them.  VALU-to-VALU dependencies need no wait states.
-__device__ __forceinline__ double log1p_horner(double r) {
-    double p;
-    asm("v_fma_f64 %0, %1, %2, %3\n\t"
-        "v_fma_f64 %0, %1, %0, %4\n\t"
-        "v_fma_f64 %0, %1, %0, %5\n\t"
-        "v_fma_f64 %0, %1, %0, %6\n\t"
-        "v_fma_f64 %0, %1, %0, %7"
-        : "=&v"(p)
-        : "v"(r), "v"(1.0 / 7.0), "s"(-1.0 / 6.0), "s"(1.0 / 5.0), "s"(-0.25), "s"(1.0 / 3.0), "s"(-0.5));
-    return p;
-}
-
-constexpr int kLogOneBin = (int)(((0x3FF00000u - 0x3FE60000u) >> 13) & 127);   // bin holding 1.0
-
-__device__ __forceinline__ double fast_log_sel(double x, bool near1, const LogTab* __restrict__ tab) {
-    const long long ix = __double_as_longlong(x);
-    const uint32_t hi = (uint32_t)(ix >> 32);
-    const int lo = (int)ix;
-    const uint32_t th = hi - (uint32_t)(kLogOff >> 32);
-    const int i = near1 ? kLogOneBin : (int)((th >> 13) & 127);
-    const int k = near1 ? 0 : ((int)th >> 20);
-    const uint32_t zh = near1 ? hi : hi - (th & 0xFFF00000u);
-    const double z = __hiloint2double((int)zh, lo);
+    const uint64_t tmp = ix - 0x3FE6000000000000ull;                  // OFF
+    const int i = (int)((tmp >> 45) & 127);
+    const int k = (int)((int64_t)tmp >> 52);
+    const double z = __builtin_bit_cast(double, ix - (tmp & 0xFFF0000000000000ull));
     const LogTab e = tab[i];
-    const double r = fma(z, e.invc, -1.0);
     const double kd = (double)k;
-    const double w = fma(kd, 0x1.62e42fefa3800p-1, e.logc);       // k*ln2_hi + log c (exact product)
-    const double hs = w + r;
-    double ls = (w - hs) + r;
-    ls = fma(kd, 0x1.ef35793c76730p-45, ls);                      // k*ln2_lo
-    const double p = log1p_horner(r);
-    return hs + fma(r * r, p, ls);                                // log1p(r) = r + r^2 P(r)
+    const double r = fma(z, e.invc, -1.0);                            // r ~= z/c - 1
+    const double w = fma(kd, kGlibcLn2Hi, e.logc);
+    const double hi = r + w;
+    const double lo = fma(kd, kGlibcLn2Lo, (w - hi) + r);
+    const double r2 = r * r;
+    const double P = fma(fma(r, kGlibcLogA[4], kGlibcLogA[3]), r2, fma(r, kGlibcLogA[2], kGlibcLogA[1]));
+    return fma(r * r2, P, fma(r2, kGlibcLogA[0], lo)) + hi;           // lo + r2 A0 + r r2 (A1 + ...) + hi
 }
 
-__device__ __forceinline__ double fast_log(double x, const LogTab* __restrict__ tab) {
-    return fast_log_sel(x, fabs(x - 1.0) < 0x1.0p-8, tab);
+// glibc's {invc, logc} table as the device keeps it (copied into each context, then into LDS by the waves that
+// run the exact loop)
+inline void glibc_log_table(LogTab* out) {
+    for (int i = 0; i < kLogTabEntries; ++i) out[i] = LogTab{kGlibcLogTab[2 * i], kGlibcLogTab[2 * i + 1]};
 }
 
-// -log(1 - U), U = u01(lo, hi): the reference's np.random.exponential(1) (gillespie_algo.py:62).
-// |(1 - U) - 1| = U < 2^-8  <=>  m < 2^45  <=>  hi >> 11 < 2^13, so the near-1 test is one integer compare.
+// -log(1 - U), U = u01(lo, hi): the reference's np.random.exponential(1) (gillespie_algo.py:62), 1 - U exact.
 __device__ __forceinline__ double neg_log_one_minus_u01(uint32_t lo, uint32_t hi, const LogTab* __restrict__ tab) {
-    return -fast_log_sel(one_minus_u01(lo, hi), (hi >> 11) < 8192u, tab);
-}
-
-// 1/a to ~1 ulp: hardware reciprocal + two Newton steps
-__device__ __forceinline__ double recip(double a) {
-    double r = __builtin_amdgcn_rcp(a);
-    r = fma(fma(-a, r, 1.0), r, r);
-    return fma(fma(-a, r, 1.0), r, r);
+    return -glibc_log(one_minus_u01(lo, hi), tab);
 }
 
 // ------------------------------------------------------------------------------- Gillespie SSA
@@ -168,13 +154,14 @@ __device__ __forceinline__ double recip(double a) {
 // Every lane still in the loop is at the same event index k (all start at 0 and step together), so k is
 // read wave-uniform: Philox's first round (and half of its second) then runs on the scalar unit.
 //
-// Fast path + certified fallback: the channel decision of the reference is
+// The clock is the reference's bit for bit: propensities in its expression order (((beta*S)*I)/N, IEEE
+// division), their builtin-sum order, scale = 1/sum (IEEE), tau = scale * -log(1 - U) with glibc's log
+// (gillespie_algo.py:37-40, :62), t + tau accumulated as :68.  So every step-boundary decision t + tau > tmax
+// (:65) is the reference's -- no tolerance.  The channel decision of the reference is
 //   count_i [ fl(c_i / c_last) <= u ],  c = cumsum(fl(a_l / sum(a)))            (numpy choice, :63)
-// whose ratios agree with q_i = (a_0 + ... + a_i) * (1/sum a) to a few ulps.  When every q_i is farther than
+// whose ratios agree with q_i = (a_0 + ... + a_i) * scale to a few ulps.  When every q_i is farther than
 // kBand from u the decision is the reference's; otherwise the reference expression is evaluated exactly
-// (IEEE divisions in the reference's order).  The event time uses 1/sum(a) and log to ~1 ulp, so the
-// clock t can differ from the reference's by ulps; a step-boundary decision can then differ only when
-// t + tau lands within a few ulps of the step end (p ~ 1e-13 per particle-step).
+// (IEEE divisions in the reference's order).
 constexpr double kBand = 0x1.0p-44;
 
 __device__ __noinline__ bool sir_channel_exact(double beta, double gamma, double S, double I, double N, double u) {
@@ -217,34 +204,36 @@ __device__ __forceinline__ int subgroups_channel_exact(const double* th, const d
 // event(r) = one pass of the reference's loop body with Philox block r (returns false, state untouched, when
 // the event overshoots tmax: the reference's break), save() back to counts.
 //
-// Propensities are formed as (beta/N) * (S*I) and with fused sums: within a few ulps of the reference's
-// ((beta*S)*I)/N and a0 + gamma*I, which the 2^-44 channel band and the ulp-level tau tolerance absorb
-// (DESIGN.md §4).
+// Propensities, their sums and tau follow the reference's expressions exactly (see above); rates() is shared by
+// event() and tau_of() (the wave-cooperative replay evaluates events' times in parallel with it).
 template <int MODEL, int G>
 struct SsaState;
 
 template <>
 struct SsaState<kSIR, 1> {                                             // gillespie_algo.py:10-75
-    double S, I, R, N, bN;
+    double S, I, R, N;
     int nrec;
-    __device__ __forceinline__ void load(const double* x, const ChainParam& cp) {
+    __device__ __forceinline__ void load(const double* x, const ChainParam&) {
         S = x[0]; I = x[1]; R = x[2];
         N = (S + I) + R;                                               // :35
-        bN = cp.theta[0] / N;
         nrec = 0;
     }
     __device__ __forceinline__ bool active() const { return I > 0.0; }   // :48
+    // a0 and scale = 1/sum(a) in the reference's order (:38-39, :62)
+    __device__ __forceinline__ double rates(const ChainParam& cp, double& a0) const {
+        a0 = ((cp.theta[0] * S) * I) / N;                              // beta * s * i / N
+        const double a1 = cp.theta[1] * I;                             // gamma * i
+        return 1.0 / (a0 + a1);                                        // 1/sum(evaluated_reactions)
+    }
     __device__ __forceinline__ bool event(const Block& r, double& t, double tmax, const ChainParam& cp,
                                           const LogTab* __restrict__ tab) {
-        const double gamma = cp.theta[1];
-        const double a0 = bN * (S * I);                                // :38
-        const double as = fma(gamma, I, a0);                           // :39
-        const double ri = recip(as);
-        const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);  // np.random.exponential, :62
+        double a0;
+        const double scale = rates(cp, a0);
+        const double tau = scale * neg_log_one_minus_u01(r.x, r.y, tab);   // np.random.exponential(scale), :62
         const double u = u01(r.z, r.w);
-        const double q = a0 * ri;
+        const double q = a0 * scale;
         bool second = q <= u;                                          // choice(2, p=a/sum(a)), :63
-        if (fabs(q - u) <= kBand) second = sir_channel_exact(cp.theta[0], gamma, S, I, N, u);
+        if (fabs(q - u) <= kBand) second = sir_channel_exact(cp.theta[0], cp.theta[1], S, I, N, u);
         const double tn = t + tau;
         if (tn > tmax) return false;                                   // :65-66
         t = tn;                                                        // :68-70; R is not needed in the loop
@@ -254,35 +243,37 @@ struct SsaState<kSIR, 1> {                                             // gilles
         return true;
     }
     __device__ __forceinline__ void save(double* x) const { x[0] = S; x[1] = I; x[2] = R + (double)nrec; }
-    // event()'s tau, same expressions (the wave-cooperative replay evaluates events' times in parallel)
+    // event()'s tau, same expressions
     __device__ __forceinline__ double tau_of(const Block& r, const ChainParam& cp, const LogTab* __restrict__ tab) const {
-        const double a0 = bN * (S * I);
-        const double as = fma(cp.theta[1], I, a0);
-        return recip(as) * neg_log_one_minus_u01(r.x, r.y, tab);
+        double a0;
+        return rates(cp, a0) * neg_log_one_minus_u01(r.x, r.y, tab);
     }
 };
 
 template <>
 struct SsaState<kSEIR, 1> {                                            // gillespie_algo.py:78-146
-    double S, E, I, R, N, bN;
-    __device__ __forceinline__ void load(const double* x, const ChainParam& cp) {
+    double S, E, I, R, N;
+    __device__ __forceinline__ void load(const double* x, const ChainParam&) {
         S = x[0]; E = x[1]; I = x[2]; R = x[3];
         N = ((S + E) + I) + R;                                         // :104
-        bN = cp.theta[0] / N;                                          // theta = (beta, alpha, gamma), :92
     }
     __device__ __forceinline__ bool active() const { return E > 0.0 || I > 0.0; }   // :119
+    // cumulative a0, a0 + a1 and scale = 1/sum(a), theta = (beta, alpha, gamma) (:92, :107-109, :133)
+    __device__ __forceinline__ double rates(const ChainParam& cp, double& a0, double& a01) const {
+        a0 = ((cp.theta[0] * S) * I) / N;
+        a01 = a0 + cp.theta[1] * E;
+        return 1.0 / (a01 + cp.theta[2] * I);
+    }
     __device__ __forceinline__ bool event(const Block& r, double& t, double tmax, const ChainParam& cp,
                                           const LogTab* __restrict__ tab) {
-        const double alpha = cp.theta[1], gamma = cp.theta[2];
-        const double a0 = bN * (S * I), a01 = fma(alpha, E, a0);       // :107-109
-        const double as = fma(gamma, I, a01);
-        const double ri = recip(as);
-        const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);  // :133
+        double a0, a01;
+        const double scale = rates(cp, a0, a01);
+        const double tau = scale * neg_log_one_minus_u01(r.x, r.y, tab);  // :133
         const double u = u01(r.z, r.w);
-        const double q0 = a0 * ri, q1 = a01 * ri;
+        const double q0 = a0 * scale, q1 = a01 * scale;
         int ch = (q0 <= u ? 1 : 0) + (q1 <= u ? 1 : 0);                // :134
         if (fabs(q0 - u) <= kBand || fabs(q1 - u) <= kBand)
-            ch = seir_channel_exact(cp.theta[0], alpha, gamma, S, E, I, N, u);
+            ch = seir_channel_exact(cp.theta[0], cp.theta[1], cp.theta[2], S, E, I, N, u);
         const double tn = t + tau;
         if (tn > tmax) return false;                                   // :136-137
         t = tn;
@@ -294,16 +285,15 @@ struct SsaState<kSEIR, 1> {                                            // gilles
     }
     __device__ __forceinline__ void save(double* x) const { x[0] = S; x[1] = E; x[2] = I; x[3] = R; }
     __device__ __forceinline__ double tau_of(const Block& r, const ChainParam& cp, const LogTab* __restrict__ tab) const {
-        const double a0 = bN * (S * I), a01 = fma(cp.theta[1], E, a0);
-        const double as = fma(cp.theta[2], I, a01);
-        return recip(as) * neg_log_one_minus_u01(r.x, r.y, tab);
+        double a0, a01;
+        return rates(cp, a0, a01) * neg_log_one_minus_u01(r.x, r.y, tab);
     }
 };
 
 template <int G>
 struct SubgroupsState {                                                // gillespie_algo.py:148-233
     static constexpr int NCH = G * G + G;
-    double S[G], I[G], R[G], sumN, invSumN;
+    double S[G], I[G], R[G], sumN;
     __device__ __forceinline__ void load(const double* x, const ChainParam&) {
         sumN = 0.0;
 #pragma unroll
@@ -311,7 +301,23 @@ struct SubgroupsState {                                                // gilles
             S[g] = x[3 * g]; I[g] = x[3 * g + 1]; R[g] = x[3 * g + 2];
             sumN = sumN + ((S[g] + I[g]) + R[g]);                      // sum(N), :176,:182
         }
-        invSumN = 1.0 / sumN;
+    }
+    // cumulative propensities in dict insertion order (s_{g}_{g2} then i_{g}, :180-185) summed as
+    // sum(list(evaluated_reactions.values())) (:208); returns 1/sum
+    __device__ __forceinline__ double rates(const ChainParam& cp, double* cum) const {
+        const double gamma = cp.theta[G * G];
+        double run = 0.0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+#pragma unroll
+            for (int g2 = 0; g2 < G; ++g2) {
+                run = run + ((cp.theta[g * G + g2] * S[g2]) * I[g]) / sumN;   // beta[g,g2] s_g2 i_g / sum(N)
+                cum[g * (G + 1) + g2] = run;
+            }
+            run = run + gamma * I[g];                                  // gamma i_g
+            cum[g * (G + 1) + G] = run;
+        }
+        return 1.0 / run;
     }
     __device__ __forceinline__ bool active() const {                   // :192-193, :222
         double infected = 0.0;
@@ -321,22 +327,9 @@ struct SubgroupsState {                                                // gilles
     }
     __device__ __forceinline__ bool event(const Block& r, double& t, double tmax, const ChainParam& cp,
                                           const LogTab* __restrict__ tab) {
-        const double gamma = cp.theta[G * G];
         double cum[NCH];
-        double run = 0.0;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {                                  // channel order, :180-185
-            const double cI = I[g] * invSumN;
-#pragma unroll
-            for (int g2 = 0; g2 < G; ++g2) {
-                run = fma(cp.theta[g * G + g2] * S[g2], cI, run);
-                cum[g * (G + 1) + g2] = run;
-            }
-            run = fma(gamma, I[g], run);
-            cum[g * (G + 1) + G] = run;
-        }
-        const double ri = recip(run);
-        const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);
+        const double ri = rates(cp, cum);
+        const double tau = ri * neg_log_one_minus_u01(r.x, r.y, tab);  // :207
         const double u = u01(r.z, r.w);
         int ch = 0;
         bool close = false;
@@ -364,16 +357,8 @@ struct SubgroupsState {                                                // gilles
         for (int g = 0; g < G; ++g) { x[3 * g] = S[g]; x[3 * g + 1] = I[g]; x[3 * g + 2] = R[g]; }
     }
     __device__ __forceinline__ double tau_of(const Block& r, const ChainParam& cp, const LogTab* __restrict__ tab) const {
-        const double gamma = cp.theta[G * G];
-        double run = 0.0;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const double cI = I[g] * invSumN;
-#pragma unroll
-            for (int g2 = 0; g2 < G; ++g2) run = fma(cp.theta[g * G + g2] * S[g2], cI, run);
-            run = fma(gamma, I[g], run);
-        }
-        return recip(run) * neg_log_one_minus_u01(r.x, r.y, tab);
+        double cum[NCH];
+        return rates(cp, cum) * neg_log_one_minus_u01(r.x, r.y, tab);
     }
 };
 template <int G> struct SsaState<kSubgroups, G> : SubgroupsState<G> {};

@@ -33,7 +33,7 @@ struct StepArgs {
     double cert_k;                // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp)
     const double* Y;
     const double* lf;
-    const LogTab* logtab;         // fast_log table [kLogTabEntries] (context-resident)
+    const LogTab* logtab;         // glibc log table [kLogTabEntries] (context-resident)
     const ChainParam* cp;
     int32_t* hidden;
     int32_t* ancestry;
@@ -67,6 +67,20 @@ struct SimArgs {
     const int32_t* in;
     int32_t* out;
     unsigned long long* events;
+};
+
+// full-path SSA (epipf_simulate_path): event-major outputs, so each loop iteration's stores are coalesced
+struct SimPathArgs {
+    const LogTab* logtab;
+    int n, cap;
+    uint32_t step;
+    double tmax;
+    const ChainParam* cp;
+    const int32_t* in;
+    double* times;               // [cap][n]
+    int32_t* states;             // [cap][C][n]
+    int32_t* nev;                // [n]
+    int32_t* final_state;        // [n][C]
 };
 
 struct ResampleArgs {
@@ -140,8 +154,8 @@ int prefix_segment(int B);
 constexpr int kMaxSegments = 200;
 hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, const FilterStreams& fs);
 hipError_t launch_path_sample(const PathArgs& a, hipStream_t s);
-hipError_t launch_log_table(LogTab* tab, hipStream_t s);
 hipError_t launch_simulate(const SimArgs& a, int model, int G, hipStream_t s);
+hipError_t launch_simulate_path(const SimPathArgs& a, int model, int G, hipStream_t s);
 hipError_t launch_resample(const ResampleArgs& a, hipStream_t s);
 hipError_t launch_abc_trials(const AbcArgs& a, hipStream_t s);
 size_t abc_sort_temp_bytes(int n);

@@ -266,9 +266,6 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
     }
 }
 
-// the fast_log table, built once per context on the device (so it uses the device log)
-__global__ void log_table_kernel(LogTab* tab) { log_table_entry(tab, threadIdx.x); }
-
 // particle_path_sampler, pmcmc.py:236-248 (one lane per chain; T dependent loads)
 __global__ void path_sample_kernel(PathArgs a) {
     const int chain = blockIdx.x * blockDim.x + threadIdx.x;
@@ -304,6 +301,51 @@ __global__ __launch_bounds__(256) void simulate_kernel(SimArgs a) {
     unsigned long long e = (unsigned long long)nev;
     for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
     if ((threadIdx.x & 63) == 0) atomicAdd(a.events, e);
+}
+
+// Full-path SSA (gillespie_algo.py *_simulate with last_values_only=False): the exact event loop -- whose clock is
+// the reference's bit for bit (SsaState) -- storing every event's time and state (:68-70).  Same draws and same
+// final state as simulate_kernel.  Lanes of a wave step together (the event index is wave-uniform), so event k's
+// stores of the wave land in contiguous [k][...][lane] rows.
+template <int MODEL, int G>
+__global__ __launch_bounds__(256) void simulate_path_kernel(SimPathArgs a) {
+    constexpr int C = Shape<MODEL, G>::C;
+    __shared__ LogTab tab[kLogTabEntries];
+    if (threadIdx.x < kLogTabEntries) tab[threadIdx.x] = a.logtab[threadIdx.x];
+    __syncthreads();
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= a.n) return;
+    const ChainParam cp = *a.cp;
+    const uint32_t ptag = (a.step & 0xFFFFFFu) | kDomainSSA;
+    double x[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = (double)a.in[(size_t)j * C + c];
+    SsaState<MODEL, G> st;
+    st.load(x, cp);
+    double t = 0.0;
+    uint32_t k = 0;
+    int nev = 0;
+    bool alive = st.active();
+    while (alive) {
+        const Block r = philox(__builtin_amdgcn_readfirstlane(k), (uint32_t)j, ptag, cp.f, cp.k0, cp.k1);
+        ++k;
+        const bool ev = st.event(r, t, a.tmax, cp, tab);
+        if (ev) {
+            if (nev < a.cap) {
+                double xs[C];
+                st.save(xs);
+                a.times[(size_t)nev * a.n + j] = t;
+#pragma unroll
+                for (int c = 0; c < C; ++c) a.states[((size_t)nev * C + c) * a.n + j] = (int32_t)xs[c];
+            }
+            ++nev;
+        }
+        alive = ev && st.active();
+    }
+    st.save(x);
+#pragma unroll
+    for (int c = 0; c < C; ++c) a.final_state[(size_t)j * C + c] = (int32_t)x[c];
+    a.nev[j] = nev;
 }
 
 // Standalone resampler over caller-supplied weights and uniforms (same scan + search code as the filter).
@@ -424,11 +466,6 @@ hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_cha
     return launch_model<64>(a, model, G, obs, n_chains, fs);
 }
 
-hipError_t launch_log_table(LogTab* tab, hipStream_t s) {
-    hipLaunchKernelGGL(log_table_kernel, dim3(1), dim3(kLogTabEntries), 0, s, tab);
-    return hipGetLastError();
-}
-
 hipError_t launch_path_sample(const PathArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(path_sample_kernel, dim3((a.n_chains + 63) / 64), dim3(64), 0, s, a);
     return hipGetLastError();
@@ -449,6 +486,27 @@ hipError_t launch_simulate(const SimArgs& a, int model, int G, hipStream_t s) {
                 case 2: sim_t<kSubgroups, 2>(a, s); break;
                 case 3: sim_t<kSubgroups, 3>(a, s); break;
                 case 4: sim_t<kSubgroups, 4>(a, s); break;
+                default: return hipErrorInvalidValue;
+            }
+    }
+    return hipGetLastError();
+}
+
+template <int MODEL, int G>
+static void sim_path_t(const SimPathArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL((simulate_path_kernel<MODEL, G>), dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+}
+
+hipError_t launch_simulate_path(const SimPathArgs& a, int model, int G, hipStream_t s) {
+    switch (model) {
+        case kSIR: sim_path_t<kSIR, 1>(a, s); break;
+        case kSEIR: sim_path_t<kSEIR, 1>(a, s); break;
+        default:
+            switch (G) {
+                case 1: sim_path_t<kSubgroups, 1>(a, s); break;
+                case 2: sim_path_t<kSubgroups, 2>(a, s); break;
+                case 3: sim_path_t<kSubgroups, 3>(a, s); break;
+                case 4: sim_path_t<kSubgroups, 4>(a, s); break;
                 default: return hipErrorInvalidValue;
             }
     }

@@ -14,7 +14,11 @@ numpy-only Dormand-Prince 5(4) with tight tolerances (agrees with odeint to ~1e-
 integer datasets match it exactly unless an ODE value sits within that distance of an integer).  The default
 picks odeint when scipy imports and dopri5 otherwise.
 """
+import os
+
 import numpy as np
+
+DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
 
 
 def differential_sir(n_sir, t, beta, gamma):
@@ -167,12 +171,14 @@ def benchmark_dataset(cfg, integrator=None):
             describe="ODE SIR y0=(4800,20,0), beta=2, gamma=1, 15 daily rows, binomial thinning p=.1 "
                      "(under-reported counts), RandomState(11)")
     if cfg == 5:
-        pop = np.array([[2000, 30, 0], [3000, 40, 0]])
-        ode = sir_subgroups_simulate_discrete(pop, np.linspace(0, 14, num=200), np.array([[5, 2], [1, 3]]), 0.5,
-                                              integrator=integrator)
-        return thin_binomial(ode[:, :6], 0.1, np.random.RandomState(14)), dict(
+        # the reference's SSA-path recipe (tests/test_simulations_subgroups.py:66-78), which writes the
+        # sir_subgrps.csv that tests/test_pmcmc_sir_subgrps.py:22 loads; generated by tests/golden/make_golden.py
+        # (the unmodified reference, np.random.seed(5)) and shipped as package data, as the reference ships its CSVs
+        Y = np.loadtxt(os.path.join(DATA_DIR, "sir_subgrps.csv"), delimiter=",")
+        return Y, dict(
             model="sir_subgroups", n_population=[2030, 3040], mu=[30, 40], theta=[4.0, 1.0, 1.0, 4.0, 1.0],
             probs=0.1, N=10000,
-            describe="ODE 2-group SIR pop=[[2000,30,0],[3000,40,0]], beta=[[5,2],[1,3]], gamma=.5, 15 daily rows, "
-                     "binomial thinning p=.1, RandomState(14)")
+            describe="2-group SIR SSA path pop=[[2000,30,0],[3000,40,0]], beta=[[5,2],[1,3]], gamma=.5, first event "
+                     "of each day 0..13, binomial thinning p=.1 (tests/test_simulations_subgroups.py:66-78, "
+                     "np.random.seed(5))")
     raise ValueError(f"unknown benchmark config {cfg}")

@@ -144,6 +144,28 @@ class Engine:
                                      ptr(ev)), "epipf_simulate")
         return out, int(ev[0])
 
+    def simulate_path(self, states, theta, max_time=1.0, key=0, filter_index=0, step=0, max_events=None):
+        """Full event paths from int states [n, C]: (times [n, cap], states [n, cap, C] int32, n_events [n],
+        final [n, C] int32); row j holds trajectory j's first n_events[j] events.  With max_events=None the buffer
+        grows to the longest path (a second call with the same draws when the first guess was short)."""
+        states = np.ascontiguousarray(np.asarray(states, dtype=np.int32).reshape(-1, self.C))
+        th, _ = theta_vector(self.model, theta)
+        th = np.ascontiguousarray(th)
+        n = states.shape[0]
+        cap = 1024 if max_events is None else int(max_events)
+        while True:
+            t = np.empty((n, max(cap, 1)))
+            x = np.empty((n, max(cap, 1), self.C), dtype=np.int32)
+            nev = np.zeros(n, dtype=np.int32)
+            fin = np.empty((n, self.C), dtype=np.int32)
+            check(self._L.epipf_simulate_path(self._h, n, ptr(states), ptr(th), th.size, float(max_time),
+                                              int(key) & (2**64 - 1), int(filter_index) & 0xFFFFFFFF, int(step), cap,
+                                              ptr(t), ptr(x), ptr(nev), ptr(fin)), "epipf_simulate_path")
+            longest = int(nev.max()) if n else 0
+            if max_events is not None or longest <= cap:
+                return t[:, :cap], x[:, :cap], nev, fin
+            cap = longest
+
     def resample(self, w, u):
         w = np.ascontiguousarray(np.asarray(w, dtype=np.float64))
         u = np.ascontiguousarray(np.asarray(u, dtype=np.float64))

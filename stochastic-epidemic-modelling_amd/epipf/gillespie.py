@@ -2,10 +2,10 @@
 
 `sir_simulate`, `seir_simulate`, `sir_subgroups_simulate` (gillespie_algo.py:10-75, 78-146, 148-233)
 with last_values_only=True propagate one state through the same kernel code the particle filter
-uses; the `*_batch` variants propagate many states in one launch (one lane per state).  Draws come
-from the keyed Philox stream: state j, event k -> counter (k, j, step, filter_index).
-Full-path mode (last_values_only=False, used by the reference's ABC sampler and plots) is not on
-the particle-filter path and is not provided by this engine.
+uses; with last_values_only=False they return the reference's full path dict (event times and the
+compartments after every event, from epipf_simulate_path).  `simulate_batch` / `simulate_path_batch`
+propagate many states in one launch (one lane per state).  Draws come from the keyed Philox stream:
+state j, event k -> counter (k, j, step, filter_index).
 """
 import numpy as np
 
@@ -28,24 +28,49 @@ def simulate_batch(type_model, states, theta, max_time=1.0, *, key=None, filter_
     return eng.simulate(np.rint(states).astype(np.int32), theta, max_time, k, f, step)
 
 
-def _full_path_unsupported():
-    raise NotImplementedError("last_values_only=False (full event path) is not part of the GPU particle-filter "
-                              "path; see DESIGN.md §8 (ABC / full-path SSA is a later row)")
+def simulate_path_batch(type_model, states, theta, max_time=1.0, *, key=None, filter_index=None, step=0, device=0):
+    """Full paths from int states [n, C]: (times [n, cap], states [n, cap, C], n_events [n], final [n, C])."""
+    from .engine import model_id, theta_vector
+    mid = model_id(type_model)
+    _, G = theta_vector(mid, theta)
+    eng = get_engine(mid, G, 1, 1, 1, device)
+    k, f = _stream(key, filter_index)
+    return eng.simulate_path(np.rint(np.asarray(states)).astype(np.int32), theta, max_time, k, f, step)
+
+
+def _path_dict(names, x0, times, states, n, time_first):
+    """The reference's conditions dict: the initial value then one entry per event (gillespie_algo.py:68-70);
+    counts keep the type of the caller's population entries, as the reference's `value + stoichiometry` does."""
+    conv = [type(v.item() if isinstance(v, np.generic) else v) for v in x0]
+    cols = {}
+    for c, name in enumerate(names):
+        cols[name] = [x0[c]] + [conv[c](v) for v in states[:n, c].tolist()]
+    tl = [0.0] + times[:n].tolist()
+    return {"time": tl, **cols} if time_first else {**cols, "time": tl}
+
+
+def _one_path(model, names, population, theta, max_time, time_first, key, filter_index, step):
+    flat = np.asarray(population, dtype=object).reshape(-1).tolist()
+    t, x, n, _ = simulate_path_batch(model, np.asarray(flat, dtype=float).reshape(1, -1), theta, max_time, key=key,
+                                     filter_index=filter_index, step=step)
+    return _path_dict(names, flat, t[0], x[0], int(n[0]), time_first)
 
 
 def sir_simulate(population, theta_proposal, max_time, last_values_only, *, key=None, filter_index=None, step=0):
-    """gillespie_algo.py:10-75 (last_values_only=True).  Returns (s, i, r) floats."""
+    """gillespie_algo.py:10-75.  last_values_only=True: (s, i, r) floats; False: the reference's
+    {"s": [...], "i": [...], "r": [...], "time": [...]} path."""
     if not last_values_only:
-        _full_path_unsupported()
+        return _one_path("sir", ("s", "i", "r"), population, theta_proposal, max_time, False, key, filter_index, step)
     out, _ = simulate_batch("sir", np.asarray(population, dtype=float).reshape(1, 3), theta_proposal, max_time,
                             key=key, filter_index=filter_index, step=step)
     return tuple(float(v) for v in out[0])
 
 
 def seir_simulate(population, theta_proposal, max_time, last_values_only, *, key=None, filter_index=None, step=0):
-    """gillespie_algo.py:78-146 (last_values_only=True).  Returns (s, e, i, r) floats."""
+    """gillespie_algo.py:78-146.  last_values_only=True: (s, e, i, r) floats; False: the reference's path dict."""
     if not last_values_only:
-        _full_path_unsupported()
+        return _one_path("seir", ("s", "e", "i", "r"), population, theta_proposal, max_time, False, key,
+                         filter_index, step)
     out, _ = simulate_batch("seir", np.asarray(population, dtype=float).reshape(1, 4), theta_proposal, max_time,
                             key=key, filter_index=filter_index, step=step)
     return tuple(float(v) for v in out[0])
@@ -53,11 +78,14 @@ def seir_simulate(population, theta_proposal, max_time, last_values_only, *, key
 
 def sir_subgroups_simulate(population, betas_proposal, gamma_proposal, max_time, last_values_only, *, key=None,
                            filter_index=None, step=0):
-    """gillespie_algo.py:148-233 (last_values_only=True).  Returns [[s, i, r] per group]."""
-    if not last_values_only:
-        _full_path_unsupported()
-    pop = np.asarray(population, dtype=float)
+    """gillespie_algo.py:148-233.  last_values_only=True: [[s, i, r] per group]; False: the reference's
+    {"time": [...], "s_0": [...], "i_0": [...], "r_0": [...], "s_1": ...} path."""
+    pop = np.asarray(population)
     G = pop.shape[0]
-    out, _ = simulate_batch("sir_subgroups", pop.reshape(1, 3 * G), (betas_proposal, gamma_proposal), max_time,
-                            key=key, filter_index=filter_index, step=step)
+    if not last_values_only:
+        names = tuple(f"{c}_{g}" for g in range(G) for c in ("s", "i", "r"))
+        return _one_path("sir_subgroups", names, pop, (betas_proposal, gamma_proposal), max_time, True, key,
+                         filter_index, step)
+    out, _ = simulate_batch("sir_subgroups", pop.astype(float).reshape(1, 3 * G), (betas_proposal, gamma_proposal),
+                            max_time, key=key, filter_index=filter_index, step=step)
     return [[float(v) for v in out[0, 3 * g:3 * g + 3]] for g in range(G)]

@@ -1,2 +1,3 @@
-"""Drop-in module mirroring the reference's gillespie_algo.py names (last_values_only=True on the GPU)."""
-from epipf.gillespie import seir_simulate, simulate_batch, sir_simulate, sir_subgroups_simulate  # noqa: F401
+"""Drop-in module mirroring the reference's gillespie_algo.py names (last-value and full-path modes on the GPU)."""
+from epipf.gillespie import (seir_simulate, simulate_batch, simulate_path_batch, sir_simulate,  # noqa: F401
+                             sir_subgroups_simulate)

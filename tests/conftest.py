@@ -64,3 +64,23 @@ def pmcmc_golden():
 def datasets_golden():
     z = np.load(os.path.join(GOLDEN, "datasets.npz"), allow_pickle=False)
     return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="session")
+def path_golden():
+    return load_golden("path_golden.npz")
+
+
+def path_rows(rec):
+    """Split a path golden's concatenated events into per-trajectory (times, rows) lists."""
+    counts = rec["counts"]
+    ends = np.cumsum(counts)
+    starts = ends - counts
+    return [(rec["times"][a:b], rec["rows"][a:b]) for a, b in zip(starts, ends)]
+
+
+def path_theta(rec):
+    th = rec["theta"]
+    if str(rec["model"]) == "sub":
+        return "sir_subgroups", (th[:4].reshape(2, 2), float(th[4]))
+    return str(rec["model"]), tuple(th)

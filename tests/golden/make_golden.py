@@ -23,8 +23,10 @@ numpy's real global RandomState, seeded with `np.random.seed(seed)`, exactly as 
 
 Datasets are synthesised with the reference's own recipes (pmcmc.py:54-113 ODE integrators plus the
 binomial-thinning / Gaussian-noise loops quoted in tests/test_pmcmc_p.py:21-29,
-tests/test_pmcmc_noisy.py:21-29, tests/test_simulations_subgroups.py:57-64) BEFORE the shim is
-installed, on seeded RandomStates.
+tests/test_pmcmc_noisy.py:21-29, tests/test_simulations_subgroups.py:57-64, and the SSA-path recipe of
+tests/test_simulations_subgroups.py:66-78 for BASELINE config 5) BEFORE the shim is installed, on seeded
+RandomStates.  Config 5's matrix is also written as the package data file the bench loads
+(stochastic-epidemic-modelling_amd/epipf/data/sir_subgrps.csv, np.savetxt as the reference writes it).
 """
 import argparse
 import math
@@ -239,7 +241,37 @@ def make_datasets(pm):
     c3 = pm.seir_simulate_discrete((9980, 0, 20, 0), np.linspace(0, 199, num=2000), 0.5, 0.2, 0.1)
     d["cfg3_ode"] = c3.iloc[:, 1:5].to_numpy(dtype=np.float64)
     d["cfg3_noisy"] = noise_normal(d["cfg3_ode"], 0.1, np.random.RandomState(3))
+    d["cfg5_ssa"] = subgroups_ssa_dataset(pm)
     return d
+
+
+CFG5_SEED = 5
+
+
+def subgroups_ssa_dataset(pm):
+    """BASELINE config 5's data by the reference's own recipe, tests/test_simulations_subgroups.py:57-78 (the
+    sir_subgrps.csv that tests/test_pmcmc_sir_subgrps.py:22 loads): one full SSA path of the 2-group model
+    (real numpy RNG, np.random.seed(CFG5_SEED)), the first event row of each day 0..13 (time floored), then
+    np.random.binomial(count, .1) per compartment, continuing the same global stream.  [14, 6]."""
+    import pandas as pd
+    population = np.array([[2000, 30, 0], [3000, 40, 0]])
+    beta = np.array([[5, 2], [1, 3]])
+    gamma, max_time, prob_obs = .5, 14, 0.1
+    np.random.seed(CFG5_SEED)
+    conditions = pm.sir_subgroups_simulate(population, beta, gamma, max_time, False)
+    data = pd.DataFrame(conditions)
+    data.time = np.floor(data.time).astype(int)
+    ids = []
+    for t in range(max_time):
+        ids.append(next(idx for idx in range(data.shape[0]) if data.loc[idx, 'time'] == t))
+    data = data.iloc[ids, :].reset_index(drop=True)
+    data2 = np.array([[0 for _ in range(data.shape[1] - 1)]])
+    for idx in range(data.shape[0]):
+        res = []
+        for c in range(1, data.shape[1]):
+            res.append(np.random.binomial(data.iloc[idx, c], prob_obs))
+        data2 = np.append(data2, np.array([res]), axis=0)
+    return data2[1:].astype(np.float64)
 
 
 # ----------------------------------------------------------------------------------- cases
@@ -326,6 +358,50 @@ def run_ssa_cases(pm, ga, out):
             out[f"ssa_{name}_{max_time}"] = dict(states=states.astype(np.int32), theta=np.array(
                 [5.0, 2.0, 1.0, 3.0, 0.5]) if theta == "sub" else np.array(theta), max_time=max_time, key=77, f=5,
                 step=3, out=np.array(res).astype(np.int32), model=name.split("_")[0])
+
+
+def run_path_cases(pm, ga, out):
+    """gillespie_algo.*_simulate(..., last_values_only=False) run unmodified under the keyed stream (direct calls:
+    trajectory j draws event k from counter (k, j, step 3, f 5)): the event times conditions["time"][1:] and the
+    compartments after every event, concatenated over trajectories with per-trajectory counts."""
+    rs = np.random.RandomState(31)
+    st = np.stack([4820 - rs.randint(1, 400, 6), rs.randint(1, 400, 6), np.zeros(6, int)], 1)
+    st[:, 2] = rs.randint(0, 200, 6)
+    st[:, 0] -= st[:, 2]
+    st = np.concatenate([st, [[10, 0, 0], [5, 1, 0], [9980, 20, 0]]])
+    se = np.stack([4800 - rs.randint(0, 300, 5), rs.randint(0, 100, 5), rs.randint(1, 100, 5), np.zeros(5, int)], 1)
+    se[0, 2] = 0
+    sg = np.array([[2000, 30, 0, 3000, 40, 0], [1900, 50, 80, 2950, 0, 90], [2030, 0, 0, 3040, 0, 0]])
+    cases = [("sir", ga.sir_simulate, st, (2.0, 1.0), (1.0, 3.5)),
+             ("sir_cfg2", ga.sir_simulate, st[-1:], (0.25, 0.1), (30.0,)),
+             ("seir", ga.seir_simulate, se, (4.0, 1.0, 1.0), (1.0, 2.0)),
+             ("sub", ga.sir_subgroups_simulate, sg, "sub", (1.0, 4.0))]
+    for name, fn, states, theta, horizons in cases:
+        for max_time in horizons:
+            S.direct = True
+            S.key = 78
+            S.f = 5
+            times, rows, counts = [], [], []
+            for j, x in enumerate(states):
+                S.p, S.j = 3, j
+                S.k = 0
+                if theta == "sub":
+                    cond = fn(x.reshape(2, 3).astype(float), SUB_THETA[0], SUB_THETA[1], max_time, False)
+                    cols = [cond[f"{c}_{g}"] for g in range(2) for c in ("s", "i", "r")]
+                else:
+                    cond = fn(list(x.astype(float)), np.array(theta), max_time, False)
+                    cols = [cond[k] for k in (("s", "i", "r") if len(x) == 3 else ("s", "e", "i", "r"))]
+                assert all(len(c) == len(cond["time"]) for c in cols) and cond["time"][0] == 0.0
+                times.extend(cond["time"][1:])
+                rows.extend(np.array(cols).T[1:].tolist())
+                counts.append(len(cond["time"]) - 1)
+            S.direct = False
+            out[f"path_{name}_{max_time}"] = dict(
+                states=states.astype(np.int32), max_time=max_time, key=78, f=5, step=3,
+                theta=np.array([5.0, 2.0, 1.0, 3.0, 0.5]) if theta == "sub" else np.array(theta),
+                times=np.array(times, dtype=np.float64), rows=np.array(rows).reshape(-1, states.shape[1]).astype(
+                    np.int32), counts=np.array(counts, dtype=np.int32), model=name.split("_")[0])
+            print(f"path {name} T={max_time}: {sum(counts)} events", flush=True)
 
 
 ABC_CASES = [
@@ -453,6 +529,9 @@ def main():
     check_numpy_identities()
     d = make_datasets(pm)
     np.savez_compressed(os.path.join(HERE, "datasets.npz"), **d)
+    data_dir = os.path.join(REPO, "stochastic-epidemic-modelling_amd", "epipf", "data")
+    os.makedirs(data_dir, exist_ok=True)
+    np.savetxt(os.path.join(data_dir, "sir_subgrps.csv"), d["cfg5_ssa"], delimiter=", ")   # :78
     pf = install_shim(pm, ga)
     ab.np = pm.np
     only = set(args.only.split(",")) if args.only else None
@@ -466,6 +545,10 @@ def main():
         run_resample_cases(out)
         run_pmf_cases(out)
         save(out, os.path.join(HERE, "kernels_golden.npz"))
+    if not only or "path" in only:
+        out = {}
+        run_path_cases(pm, ga, out)
+        save(out, os.path.join(HERE, "path_golden.npz"))
     if not only or "pmcmc" in only:
         out = {}
         run_pmcmc_cases(pm, d, out)
