@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void abc_trials_kernel(AbcArgs a) {
             rn = philox(__builtin_amdgcn_readfirstlane(k), t, kDomainAbcSsa, a.f, a.k0, a.k1);
             const double S0 = st.S, I0 = st.I;
             const int rec0 = st.nrec;
-            const bool ev = st.event(r, clock, last_day, cp, tab);   // false: the event lands after day T-1
+            const bool ev = st.template event<true>(r, clock, last_day, cp, tab);   // false: the event lands after day T-1
             if (ev) {
                 ++nev;
                 while (next_day < clock) {                               // days the event does not reach

@@ -222,9 +222,11 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
         free_ctx(c);
         return fail(EPIPF_EHIP, "hipEventCreate failed");
     }
-    LogTab lt[kLogTabEntries];
+    // on the context stream (a NULL-stream copy would take one of the process's hardware queues, which the
+    // chain-group streams then share: two groups serialised, -14% at config 2)
+    LogTab lt[kLogTabEntries];                 // synchronised below, before it goes out of scope
     glibc_log_table(lt);
-    if (hipMemcpy(c->logtab, lt, sizeof lt, hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMemcpyAsync(c->logtab, lt, sizeof lt, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
         hipMemsetAsync(c->counters, 0, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
         free_ctx(c);
@@ -557,7 +559,7 @@ int epipf_glibc_log(int64_t n, const double* x, double* out) {
     if (n < 0 || (n > 0 && (!x || !out))) return fail(EPIPF_EINVAL, "NULL argument");
     LogTab lt[kLogTabEntries];
     glibc_log_table(lt);
-    for (int64_t i = 0; i < n; ++i) out[i] = glibc_log(x[i], lt);
+    for (int64_t i = 0; i < n; ++i) out[i] = glibc_log_impl(x[i], lt);
     return EPIPF_OK;
 }
 

@@ -96,7 +96,7 @@ constexpr uint32_t kChainFastSsa = 1u;   // (all models)
 struct LogTab { double invc, logc; };
 constexpr int kLogTabEntries = 128;
 
-__host__ __device__ inline double glibc_log(double x, const LogTab* __restrict__ tab) {
+__host__ __device__ inline double glibc_log_impl(double x, const LogTab* __restrict__ tab) {
     const uint64_t ix = __builtin_bit_cast(uint64_t, x);
     constexpr uint64_t LO = 0x3FEE000000000000ull;                    // asuint64(1 - 0x1p-4)
     constexpr uint64_t HI = 0x3FF1090000000000ull;                    // asuint64(1 + 0x1.09p-4)
@@ -136,6 +136,12 @@ __host__ __device__ inline double glibc_log(double x, const LogTab* __restrict__
     return fma(r * r2, P, fma(r2, kGlibcLogA[0], lo)) + hi;           // lo + r2 A0 + r r2 (A1 + ...) + hi
 }
 
+// The step kernels call it out of line: it runs only on their exact path (replays, ~1% of waves), and inlined, its
+// constants and branches raised the whole kernel's SGPR spills from 15 to 44 (reloads every step: -2% at config 2).
+// The ABC trial loop, where every event takes it, inlines it (glibc_log_inl).
+__device__ __noinline__ double glibc_log(double x, const LogTab* __restrict__ tab) { return glibc_log_impl(x, tab); }
+__device__ __forceinline__ double glibc_log_inl(double x, const LogTab* __restrict__ tab) { return glibc_log_impl(x, tab); }
+
 // glibc's {invc, logc} table as the device keeps it (copied into each context, then into LDS by the waves that
 // run the exact loop)
 inline void glibc_log_table(LogTab* out) {
@@ -143,8 +149,11 @@ inline void glibc_log_table(LogTab* out) {
 }
 
 // -log(1 - U), U = u01(lo, hi): the reference's np.random.exponential(1) (gillespie_algo.py:62), 1 - U exact.
+// INL: inline the log (the ABC trial loop) instead of calling it.
+template <bool INL = false>
 __device__ __forceinline__ double neg_log_one_minus_u01(uint32_t lo, uint32_t hi, const LogTab* __restrict__ tab) {
-    return -glibc_log(one_minus_u01(lo, hi), tab);
+    const double x = one_minus_u01(lo, hi);
+    return -(INL ? glibc_log_inl(x, tab) : glibc_log(x, tab));
 }
 
 // ------------------------------------------------------------------------------- Gillespie SSA
@@ -225,11 +234,12 @@ struct SsaState<kSIR, 1> {                                             // gilles
         const double a1 = cp.theta[1] * I;                             // gamma * i
         return 1.0 / (a0 + a1);                                        // 1/sum(evaluated_reactions)
     }
+    template <bool INL = false>
     __device__ __forceinline__ bool event(const Block& r, double& t, double tmax, const ChainParam& cp,
                                           const LogTab* __restrict__ tab) {
         double a0;
         const double scale = rates(cp, a0);
-        const double tau = scale * neg_log_one_minus_u01(r.x, r.y, tab);   // np.random.exponential(scale), :62
+        const double tau = scale * neg_log_one_minus_u01<INL>(r.x, r.y, tab);   // np.random.exponential(scale), :62
         const double u = u01(r.z, r.w);
         const double q = a0 * scale;
         bool second = q <= u;                                          // choice(2, p=a/sum(a)), :63
