@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define EPIPF_ABI_VERSION 4
+#define EPIPF_ABI_VERSION 5
 
 /* return codes */
 #define EPIPF_OK 0
@@ -89,6 +89,9 @@ typedef struct {
                                     group's own stream (profiling on) */
     int64_t step_kernel_launches;/* their number: one step of all chains (step_ms) is one launch per chain group on
                                     concurrent streams (EPIPF_STREAMS, default 4) */
+    int64_t last_lanes;          /* SSA lanes per particle of the last epipf_run (1: one-lane step kernel; 2..16: the
+                                    lane-group step kernel, epipf_set_lanes) */
+    int64_t last_lane_events;    /* events per lane per chunk of that run's lane-group kernel (1 for the one-lane one) */
 } epipf_stats;
 
 /* groups: G for the subgroup models (1 <= G <= 4), ignored (1) for SIR/SEIR.
@@ -180,6 +183,12 @@ int epipf_set_profiling(epipf_ctx* ctx, int level);
    Engine tuning only, no reference counterpart; results do not depend on it.  A host that runs several contexts
    from separate threads (MH iterations pipelined with the device, epipf.pmcmc.run_pipelined) sets 1 each. */
 int epipf_set_streams(epipf_ctx* ctx, int n_streams);
+/* Lanes per particle in the step kernel's SSA: 0 = automatic (default; EPIPF_LANES overrides), 1 = one lane per
+   particle (throughput: batches that fill the chip), 2/4/8/16 = a group of lanes draws consecutive events' Philox
+   blocks in parallel and runs only the sequential decisions event by event (latency: a single chain or a few chains,
+   DESIGN.md §12).  events_per_lane: events each lane of a group draws per chunk (0 = automatic).  Engine tuning only,
+   no reference counterpart; results are identical for every value. */
+int epipf_set_lanes(epipf_ctx* ctx, int lanes, int events_per_lane);
 int epipf_get_stats(epipf_ctx* ctx, epipf_stats* out);
 int epipf_reset_stats(epipf_ctx* ctx);
 

@@ -96,7 +96,25 @@ struct epipf_ctx {
     hipEvent_t gb[kMaxFilterStreams] = {};   // per-group step spans (timing)
     hipEvent_t ge[kMaxFilterStreams] = {};
     int last_groups = 1;
+    int lanes = 0;           // SSA lanes per particle: 0 = automatic (pick_lanes), else 1/2/4/8/16 (EPIPF_LANES)
+    int lane_events = 0;     // events per lane per chunk of the lane-group kernel: 0 = automatic (EPIPF_LANE_EVENTS)
+    int lane_blocks = 1280;  // automatic choice: lane groups up to this many particle blocks per launch
 };
+
+// Lanes per particle for a run of n_chains filters.  The one-lane kernel needs ~20k waves per launch to fill the
+// chip; below 8 chains of 10^4 particles (n_chains x B <= 1280 particle blocks) the lane-group kernel with W = 4
+// runs each particle-step 1.6-2.1x faster (1-8 chains, BASELINE configs 2 and 5: profiles/r2e_lanes_sweep*.jsonl;
+// W = 2, 8, 16 and K > 1 measured no better).
+static int pick_lanes(const epipf_ctx* c, int n_chains) {
+    if (c->lanes > 0) return c->lanes;
+    return (long)n_chains * c->B <= (long)c->lane_blocks ? 4 : 1;
+}
+
+static int pick_lane_events(const epipf_ctx* c, int W) {
+    if (W <= 1) return 1;
+    if (c->lane_events > 0 && group_shape_supported(W, c->lane_events)) return c->lane_events;
+    return 1;                                       // K > 1 measured no faster (profiles/r2e_lanes_sweep.jsonl)
+}
 
 // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp): D bounds the depth of the parallel
 // reduction tree behind every prefix: in-block scan (6 shuffle levels + <=4 wave offsets + 1) = 11 <= 16,
@@ -181,6 +199,12 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     if (const char* e = getenv("EPIPF_SSA_FAST")) c->fast_ssa = atoi(e) != 0;
     if (const char* e = getenv("EPIPF_CLOCK_SLACK")) c->clock_slack = std::max(1.0f, std::min(1e6f, (float)atof(e)));
     if (const char* e = getenv("EPIPF_STREAMS")) c->n_streams = std::max(1, std::min(kMaxFilterStreams, atoi(e)));
+    if (const char* e = getenv("EPIPF_LANES")) {
+        const int w = atoi(e);
+        if (w == 0 || w == 1 || w == 2 || w == 4 || w == 8 || w == 16) c->lanes = w;
+    }
+    if (const char* e = getenv("EPIPF_LANE_BLOCKS")) c->lane_blocks = std::max(0, atoi(e));
+    if (const char* e = getenv("EPIPF_LANE_EVENTS")) c->lane_events = std::max(0, atoi(e));
     c->B = (n_particles + c->wg - 1) / c->wg;
     if (step_lds_bytes(c->B, c->wg) > 160 * 1024) {
         free_ctx(c);
@@ -331,6 +355,12 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     a.wraw = c->wraw; a.wloc = c->wloc; a.bsum = c->bsum; a.log_zeta = c->log_zeta; a.status = c->status;
     a.seg = prefix_segment(c->B); a.nseg = (c->B + a.seg - 1) / a.seg;
     a.counters = c->counters;
+    a.lanes = pick_lanes(c, n_chains);
+    a.lane_events = pick_lane_events(c, a.lanes);
+    if (a.lanes > 1 && !group_shape_supported(a.lanes, a.lane_events))
+        return fail(EPIPF_EINVAL, "no lane-group kernel for %d lanes x %d events", a.lanes, a.lane_events);
+    c->stats.last_lanes = a.lanes;
+    c->stats.last_lane_events = a.lane_events;
     for (int g = 0; g < kMaxG; ++g) { a.npop[g] = c->npop[g]; a.mu[g] = c->mu[g]; a.emu[g] = c->emu[g]; a.kmax[g] = c->kmax[g]; }
 
     FilterStreams fs{};
@@ -842,6 +872,18 @@ int epipf_set_streams(epipf_ctx* c, int n_streams) {
     if (n_streams < 1 || n_streams > kMaxFilterStreams)
         return fail(EPIPF_EINVAL, "n_streams %d outside [1, %d]", n_streams, kMaxFilterStreams);
     c->n_streams = n_streams;     // streams are created at the first run that uses them
+    return EPIPF_OK;
+}
+
+int epipf_set_lanes(epipf_ctx* c, int lanes, int events_per_lane) {
+    if (!c) return fail(EPIPF_EINVAL, "NULL context");
+    if (!(lanes == 0 || lanes == 1 || lanes == 2 || lanes == 4 || lanes == 8 || lanes == 16))
+        return fail(EPIPF_EINVAL, "lanes %d not in {0 (automatic), 1, 2, 4, 8, 16}", lanes);
+    if (events_per_lane < 0) return fail(EPIPF_EINVAL, "events_per_lane %d < 0", events_per_lane);
+    if (lanes > 1 && events_per_lane > 0 && !group_shape_supported(lanes, events_per_lane))
+        return fail(EPIPF_EINVAL, "no lane-group kernel for %d lanes x %d events per lane", lanes, events_per_lane);
+    c->lanes = lanes;
+    c->lane_events = events_per_lane;
     return EPIPF_OK;
 }
 

@@ -1,0 +1,405 @@
+// epipf_group.hpp -- the lane-group step kernel: W lanes per particle, for runs too small to fill the chip.
+//
+// One chain of N = 10^4 particles is 157 waves on 1024 SIMDs, so the one-lane-per-particle step kernel
+// (epipf_kernels.hip) is latency-bound there: each SIMD runs one lone wave whose particles step through their
+// events one dependent instruction at a time.  Philox being counter-based, a particle's events do
+// not have to be drawn one after the other: a group of W lanes (W = 2, 4, 8, 16) draws W consecutive events'
+// blocks at once, and only what really is sequential runs event by event --
+//   1. lane i of the group draws the Philox block of event base + i;
+//   2. a pass over the W events in order applies the channel decisions (the certified f32 test with its exact
+//      fallback: the exact loop's decisions) on registers every lane of the group holds; lane i
+//      keeps the state before event base + i;
+//   3. lane i evaluates its event's time with the exact loop's own expressions (SsaState::tau_of: reference-order
+//      propensities, IEEE divisions, glibc's log);
+//   4. a pass adds the times in event order and stops at the first t + tau > tmax, as the exact loop does.
+// This is the wave-cooperative replay (coop_replay, epipf_device.hpp) with groups of W lanes instead of the whole
+// wave: the result is the exact loop's bit for bit, with no f32 clock to certify and therefore no replays.  The
+// in-group broadcasts of steps 2 and 4 are DPP moves (quad_perm for W <= 4, gfx950's row_newbcast for 8 and 16),
+// not LDS traffic.  Per event a group spends ~1/W of a Philox block plus the two short sequential passes, so a
+// particle advances 3-6x faster than on one lane, at W times the lanes: the right trade exactly when the chip has
+// idle SIMDs (the host picks W from chains x particles, epipf_api.cpp).
+//
+// Block = W waves, 64 particles (the same particle blocks, block sums and in-block prefixes as the one-lane
+// kernel, so resampling, weights and scans are the same code on the same values):
+//   wave 0   scan of the block sums, resampling draw + certified search (+ exact fallback), ancestor, parent
+//            rows into LDS                                                        (pmcmc.py:183-199)
+//   all      group SSA of the 64 particles (wave w, group g: particle w * 64/W + g) (gillespie_algo.py)
+//   wave 0   store the new states, weights against Y[p], in-block scan, block sum  (pmcmc.py:178-181, 222-231)
+// (A variant with one-wave workgroups of 64/W particles, spreading a chain's groups over every CU with the in-block
+// scan in a second launch, measured 5-20% slower: the step is bound by each wave's own instruction stream, not by
+// waves sharing a SIMD; profiles/r2e_lanes_sweep_onewave.jsonl.)
+#pragma once
+#include "epipf_step.hpp"
+
+#include <type_traits>
+
+#include "epipf_internal.hpp"
+
+namespace epipf {
+
+// Value of lane I of this lane's group of W consecutive lanes: DPP moves (groups of W <= 16 lie inside one DPP row).
+template <int W, int I>
+__device__ __forceinline__ uint32_t group_lane_dpp(uint32_t v) {
+    static_assert(I >= 0 && I < W, "lane inside the group");
+    if constexpr (W == 16) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + I, 0xF, 0xF, false);       // row_newbcast:I
+    } else if constexpr (W == 8) {                                      // two groups per row: one bank pair each
+        const int lo = __builtin_amdgcn_update_dpp(0, (int)v, 0x150 + I, 0xF, 0x3, false);
+        return (uint32_t)__builtin_amdgcn_update_dpp(lo, (int)v, 0x150 + 8 + I, 0xF, 0xC, false);
+    } else if constexpr (W == 4) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, I | (I << 2) | (I << 4) | (I << 6), 0xF, 0xF, false);
+    } else {
+        static_assert(W == 2, "W in {2, 4, 8, 16}");
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, I | (I << 2) | ((2 + I) << 4) | ((2 + I) << 6), 0xF,
+                                                     0xF, false);
+    }
+}
+
+// for (I = 0; I < W && f(I); ++I) with I a constant expression in f (the DPP control is an immediate), unrolled
+// in the source: the compiler declines to unroll the larger models' passes itself.
+template <int I, int W>
+struct StaticFor {
+    template <class Fn>
+    __device__ __forceinline__ static void run(Fn& f) {
+        if (f(std::integral_constant<int, I>{})) StaticFor<I + 1, W>::run(f);
+    }
+};
+template <int W>
+struct StaticFor<W, W> {
+    template <class Fn>
+    __device__ __forceinline__ static void run(Fn&) {}
+};
+
+template <int W, int I>
+__device__ __forceinline__ double group_lane_f64(double v) {
+    const uint64_t b = __double_as_longlong(v);
+    const uint32_t lo = group_lane_dpp<W, I>((uint32_t)b), hi = group_lane_dpp<W, I>((uint32_t)(b >> 32));
+    return __longlong_as_double(((uint64_t)hi << 32) | lo);
+}
+
+// Channel decision of one event on the f32 state without the exact fallback: the certified test in its product form
+// (c_i against T = uc * total, the band scaled by total: within the band of every model, FastSsa / DESIGN.md §4),
+// with `close` raised when the test cannot certify (the caller then redoes the chunk on the exact fallback).  No
+// branch: the lane-group pass runs it once per event on its critical path.
+template <typename F>
+__device__ __forceinline__ int channel_flagged(const F& st, float uc, bool& close) {
+    constexpr int NCH = F::NCH;
+    float c[NCH - 1];
+    const float total = st.cum(c);
+    const float T = uc * total, band = F::kBand * total;
+    int ch = 0;
+    bool sure = true;
+#pragma unroll
+    for (int i = 0; i < NCH - 1; ++i) {
+        ch += (c[i] < T) ? 1 : 0;
+        sure = sure && (fabsf(c[i] - T) > band);
+    }
+    close = close || (st.active() && !sure);
+    return ch;
+}
+
+// 1/sum(a) of the exact state (the reference's expressions, SsaState::rates)
+template <int MODEL, int G>
+__device__ __forceinline__ double exact_scale(const SsaState<MODEL, G>& ex, const ChainParam& cp) {
+    if constexpr (MODEL == kSIR) {
+        double a0;
+        return ex.rates(cp, a0);
+    } else if constexpr (MODEL == kSEIR) {
+        double a0, a01;
+        return ex.rates(cp, a0, a01);
+    } else {
+        double cum[SsaState<MODEL, G>::NCH];
+        return ex.rates(cp, cum);
+    }
+}
+
+// One particle over [0, tmax] by its group of W lanes, K events per lane per chunk (call with the whole group
+// active; every lane passes the same parent state x0).  Returns the number of events and the new state in xout, in
+// every lane of the group.  Bit-identical to exact_propagate (and so to the one-lane kernel).
+//
+// Chunk of E = W K events, event e drawn by lane e % W in its slot e / W:
+//   per lane, independent of the state: K Philox blocks, their channel uniforms uc and -log(1 - U) (glibc's log);
+//   pass: E channel decisions in order, branch-free (channel_flagged); lane e % W keeps the state before event e;
+//   after: the first event whose state is extinct (ballots) -> events in the chunk; if any decision was not
+//          certified, the pass is redone with the exact fallback per event;
+//   per lane: each kept state's 1/sum(a) (two IEEE divisions) times its -log(1 - U) = tau (SsaState::tau_of's
+//          expression);
+//   clock: t + tau in event order, stop at the first t + tau > tmax.
+template <int MODEL, int G, int W, int K>
+__device__ __forceinline__ int group_propagate(const double* x0, double* xout, const ChainParam& cp, uint32_t j,
+                                               uint32_t ptag, double tmax, const LogTab* __restrict__ tab) {
+    using F = FastSsa<MODEL, G>;
+    constexpr int C = Shape<MODEL, G>::C;
+    constexpr int E = W * K;
+    const int lane = (int)(threadIdx.x & 63);
+    const int gl = lane & (W - 1), gb = lane - gl;
+    F st;
+    if (!(cp.flags & kChainFastSsa) || !st.load(x0, cp)) {
+        // outside the f32 channel test's range (or EPIPF_SSA_FAST=0): the exact loop, run by every lane of the group
+        // (same result in each); the lanes here all start at event 0 together, so its event index stays uniform
+#pragma unroll
+        for (int c = 0; c < C; ++c) xout[c] = x0[c];
+        int it = 0;
+        return exact_propagate<MODEL, G>(xout, cp, j, ptag, tmax, tab, it);
+    }
+    // xout = the state s of group lane `own` (relative to the parent x0), in every lane of the group
+    auto put = [&](const F& s, int own) __attribute__((always_inline)) {
+        double xs[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) xs[c] = x0[c];
+        s.save(xs);
+#pragma unroll
+        for (int c = 0; c < C; ++c) xout[c] = (double)__shfl((int)xs[c], gb + own, 64);
+    };
+    double t = 0.0;
+    uint32_t base = 0;
+    int nev = 0;
+    if (!st.active()) {
+        put(st, 0);
+        return 0;
+    }
+    F mine[K];                                           // mine[k]: state before event k W + gl
+    for (;;) {
+        Block r[K];
+        float uc[K];
+        double L[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            r[k] = philox(base + (uint32_t)(k * W + gl), j, ptag, cp.f, cp.k0, cp.k1);
+            uc[k] = __uint_as_float(0x3F800000u | (r[k].w >> 9)) - (1.0f - kUlpF);       // uf + 2^-24
+            L[k] = neg_log_one_minus_u01<true>(r[k].x, r[k].y, tab);                     // -log(1 - U), :62
+        }
+        const F st0 = st;
+        bool close = false;
+        auto decide = [&](auto I) __attribute__((always_inline)) -> bool {
+            constexpr int e = decltype(I)::value;
+            if (gl == e % W) mine[e / W] = st;
+            const float u = __uint_as_float(group_lane_dpp<W, e % W>(__float_as_uint(uc[e / W])));
+            st.apply(channel_flagged(st, u, close), 1.f);
+            return true;
+        };
+        StaticFor<0, E>::run(decide);
+        // events up to extinction: the first e whose state before it is extinct (the last applied event emptied it)
+        int nk = E;
+#pragma unroll
+        for (int k = K - 1; k >= 0; --k) {
+            const uint64_t dead = __ballot(!mine[k].active());
+            const uint32_t bits = (uint32_t)(dead >> gb) & ((1u << W) - 1u);
+            if (bits) nk = min(nk, k * W + (int)__builtin_ctz(bits));
+        }
+        if (__ballot(close) >> gb & ((1ull << W) - 1ull)) {      // group-uniform, rare: redo with the exact fallback
+            st = st0;
+            nk = E;
+            auto decide_exact = [&](auto I) __attribute__((always_inline)) -> bool {
+                constexpr int e = decltype(I)::value;
+                if (gl == e % W) mine[e / W] = st;
+                const uint32_t rz = group_lane_dpp<W, e % W>(r[e / W].z), rw = group_lane_dpp<W, e % W>(r[e / W].w);
+                st.apply(fast_channel(st, cp, rz, rw), 1.f);
+                if (st.active()) return true;
+                nk = e + 1;
+                return false;
+            };
+            StaticFor<0, E>::run(decide_exact);
+#pragma unroll
+            for (int k = 0; k < K; ++k)                  // the state before event nk (< E): the extinct one
+                if (k * W + gl == nk) mine[k] = st;
+        }
+        double tau[K];                                   // each event's time, the exact loop's expressions
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            tau[k] = 0.0;
+            if (k * W + gl < nk) {
+                double xk[C];
+#pragma unroll
+                for (int c = 0; c < C; ++c) xk[c] = x0[c];
+                mine[k].save(xk);
+                SsaState<MODEL, G> ex;
+                ex.load(xk, cp);
+                tau[k] = exact_scale<MODEL, G>(ex, cp) * L[k];
+            }
+        }
+        // t + tau in event order (the exact loop's additions); the step ends at the first t + tau > tmax.  Branch-free:
+        // the sum runs on through the chunk (events past nk add tau = 0) and `inside` counts the events before the
+        // first overshoot -- once an event overshoots, t is no longer needed (the step ends in this chunk).
+        double tt = t;
+        int inside = 0;
+        bool alive = true;
+        auto clock = [&](auto I) __attribute__((always_inline)) -> bool {
+            constexpr int e = decltype(I)::value;
+            const uint64_t b = __double_as_longlong(tau[e / W]);
+            const uint32_t lo = group_lane_dpp<W, e % W>((uint32_t)b), hi = group_lane_dpp<W, e % W>((uint32_t)(b >> 32));
+            tt = tt + __longlong_as_double(((uint64_t)hi << 32) | lo);
+            alive = alive && !(tt > tmax);                   // :65-66
+            inside += alive ? 1 : 0;
+            return true;
+        };
+        StaticFor<0, E>::run(clock);
+        const int stop = inside < nk ? inside : -1;
+        t = tt;
+        if (stop >= 0 || nk < E) {                       // the step ends before event `end` (past tmax or extinct)
+            const int end = stop >= 0 ? stop : nk;
+            F fin = st;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (k * W + gl == end) fin = mine[k];
+            put(fin, end % W);
+            return nev + end;
+        }
+        nev += E;
+        base += (uint32_t)E;
+        if (!st.active()) {                              // extinct after the chunk's last event
+            put(st, 0);
+            return nev;
+        }
+    }
+}
+
+// LDS of the lane-group step kernel: log table | red[16] | particle rows [64][C] int32 | block-sum prefix
+inline size_t group_lds_bytes_impl(int B, int C) { return step_lds_bytes(B, 64) + sizeof(int32_t) * 64 * (size_t)C; }
+
+template <int MODEL, int G, int OBS, int W, int K>
+__global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p) {
+    using Sh = Shape<MODEL, G>;
+    constexpr int C = Sh::C;
+    constexpr int PPW = 64 / W;                          // particles per wave
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    LogTab* tab = reinterpret_cast<LogTab*>(smem);
+    double* red = smem + 2 * kLogTabEntries;             // [0]: the step's weight total, for every wave
+    int32_t* rows = reinterpret_cast<int32_t*>(red + 16);
+    double* seg_start = red + 16 + (64 * C + 1) / 2;
+    double* seg_end = seg_start + a.nseg;
+    const int chain = a.chain0 + (int)blockIdx.y;
+    const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    if (a.status[chain] != 0) return;
+    const ChainParam cp = a.cp[chain];
+    const int prev = (p - 1) & 1, cur = p & 1;
+    const size_t wprev = ((size_t)prev * a.max_chains + chain) * a.wstride;
+    const size_t wcur = ((size_t)cur * a.max_chains + chain) * a.wstride;
+    const size_t bprev = ((size_t)prev * a.max_chains + chain) * a.bstride;
+    const size_t bcur = ((size_t)cur * a.max_chains + chain) * a.bstride;
+    for (int i = (int)threadIdx.x; i < kLogTabEntries; i += 64 * W) tab[i] = a.logtab[i];
+
+    if (wave == 0) {                                     // likelihood, resampling, gather: pf_step_kernel's code
+        const int j = (int)blockIdx.x * 64 + lane;
+        const double total = (a.seg == 1)
+                                 ? scan_block_sums<64, true>(a.bsum + bprev, a.B, seg_start + a.B, seg_start, red)
+                                 : scan_segments<true>(a.bsum + bprev, a.B, a.seg, a.nseg, seg_start, seg_end);
+        if (lane == 0) red[0] = total;
+        if (total > 0.0) {
+            if (blockIdx.x == 0 && lane == 0)            // pmcmc.py:183, in log space
+                a.log_zeta[(size_t)chain * a.T + p] = a.log_zeta[(size_t)chain * a.T + p - 1] + log(total / (double)a.N);
+            double U = 0.0;
+            int anc = 0;
+            bool certified = true;
+            if (j < a.N) {                               // pmcmc.py:188-190
+                const uint32_t rtag = ((uint32_t)p & 0xFFFFFFu) | kDomainResample;
+                if (a.resample_mode == 0) {
+                    const Block r = philox(0u, (uint32_t)j, rtag, cp.f, cp.k0, cp.k1);
+                    U = u01(r.x, r.y);
+                } else {
+                    const Block r = philox(0u, 0u, rtag, cp.f, cp.k0, cp.k1);
+                    U = ((double)j + u01(r.x, r.y)) / (double)a.N;
+                }
+                if (a.seg == 1)
+                    anc = resample_search<64>(U, seg_start + a.B, seg_start, a.B, total, a.wloc + wprev, a.N, a.cert_k,
+                                              certified);
+                else
+                    anc = resample_search_seg(U, seg_start, seg_end, a.nseg, a.seg, a.bsum + bprev, a.B, total,
+                                              a.wloc + wprev, 64, a.N, a.cert_k, certified);
+            }
+            if (__any(!certified)) {
+                const int e = resample_exact_wave(!certified, U, a.wraw + wprev, a.N);
+                if (!certified) {
+                    anc = e;
+                    atomicAdd(counter_slot(a.counters) + 1, 1ull);
+                }
+            }
+            if (j < a.N) {                               // :193-199
+                anc = min(max(anc, 0), a.N - 1);
+                a.ancestry[(size_t)chain * a.anc_stride + (size_t)p * a.N + j] = anc;
+                const int32_t* hp = a.hidden + (size_t)chain * a.hist_stride + ((size_t)(p - 1) * a.N + anc) * C;
+#pragma unroll
+                for (int c = 0; c < C; ++c) rows[lane * C + c] = hp[c];
+            }
+        } else if (blockIdx.x == 0 && lane == 0) {       // all weights 0 or NaN: :187-192
+            a.status[chain] = 1;
+            a.log_zeta[(size_t)chain * a.T + p] = -__builtin_inf();
+        }
+    }
+    __syncthreads();
+    if (!(red[0] > 0.0)) return;                         // block-uniform
+
+    // group SSA: wave w, group g runs particle w * PPW + g of the block
+    const int gl = lane & (W - 1);
+    const int pl = wave * PPW + lane / W;
+    const int jg = (int)blockIdx.x * 64 + pl;
+    int nev = 0;
+    double x[C];
+    if (jg < a.N) {                                      // group-uniform
+        double x0[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) x0[c] = (double)rows[pl * C + c];
+        const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
+        nev = group_propagate<MODEL, G, W, K>(x0, x, cp, (uint32_t)jg, ptag, 1.0, tab);
+    }
+    __syncthreads();                                     // every group has read its parent row
+    if (jg < a.N && gl == 0) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) rows[pl * C + c] = (int32_t)x[c];
+    }
+    if (a.count_events) {                                // events (no lane-use figure in this kernel)
+        unsigned long long e = gl == 0 ? (unsigned long long)nev : 0ull;
+        for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
+        if (lane == 0) atomicAdd(counter_slot(a.counters), e);
+    }
+    __syncthreads();
+
+    if (wave == 0) {                                     // store, weights for step p+1, in-block scan
+        const int j = (int)blockIdx.x * 64 + lane;
+        double w = 0.0;
+        if (j < a.N) {
+            double xs[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) xs[c] = (double)rows[lane * C + c];
+            int32_t* hc = a.hidden + (size_t)chain * a.hist_stride + ((size_t)p * a.N + j) * C;
+#pragma unroll
+            for (int c = 0; c < C; ++c) hc[c] = (int32_t)xs[c];                       // :222-231
+            if (p + 1 < a.T) w = particle_weight<MODEL, G, OBS>(xs, a.Y + (size_t)p * Sh::K, cp, a.lf, a.lf_max);
+        }
+        if (p + 1 < a.T) {
+            const double loc = block_inclusive_scan<64>(w, red);
+            a.wraw[wcur + j] = w;
+            a.wloc[wcur + j] = loc;
+            if (lane == 63) a.bsum[bcur + blockIdx.x] = loc;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------- launch table
+template <int MODEL, int G, int OBS, int W, int K>
+static void launch_group_t(const StepArgs& a, int p, dim3 grid, size_t lds, hipStream_t s) {
+    hipLaunchKernelGGL((pf_step_group_kernel<MODEL, G, OBS, W, K>), grid, dim3(64 * W), lds, s, a, p);
+}
+
+// (lanes per particle W, events per lane per chunk K) instantiated
+#define EPIPF_GROUP_SHAPES(X) X(2, 1) X(4, 1) X(8, 1) X(16, 1)
+
+template <int MODEL, int G, int OBS>
+static GroupStepFn pick_wk(int W, int K) {
+#define EPIPF_PICK(w, k) if (W == w && K == k) return launch_group_t<MODEL, G, OBS, w, k>;
+    EPIPF_GROUP_SHAPES(EPIPF_PICK)
+#undef EPIPF_PICK
+    return nullptr;
+}
+
+template <int MODEL, int G>
+static GroupStepFn pick_obs(int obs, int W, int K) {
+    return obs == kBinomial ? pick_wk<MODEL, G, kBinomial>(W, K) : pick_wk<MODEL, G, kNormal>(W, K);
+}
+
+// per-model tables, one translation unit each (parallel builds)
+GroupStepFn group_launcher_sir(int model, int obs, int W, int K);
+GroupStepFn group_launcher_sub(int G, int obs, int W, int K);
+GroupStepFn group_launcher_sub2(int G, int obs, int W, int K);
+
+}  // namespace epipf

@@ -28,6 +28,8 @@ __device__ __forceinline__ unsigned long long* counter_slot(unsigned long long* 
 struct StepArgs {
     int N, T, B, wg, max_chains, resample_mode, count_events, lf_max;
     int chain0;                   // first chain of this launch (chain groups run on separate streams)
+    int lanes;                    // lanes per particle in the SSA: 1 = pf_step_kernel, 2..16 = pf_step_group_kernel
+    int lane_events;              // pf_step_group_kernel: events per lane per chunk
     int seg, nseg;                // block-sum prefix: S blocks per segment, ceil(B / S) segments (<= kMaxSegments)
     size_t hist_stride, anc_stride, wstride, bstride;
     double cert_k;                // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp)
@@ -150,6 +152,11 @@ struct FilterStreams {
 };
 
 size_t step_lds_bytes(int B, int wg);
+// lane-group step kernel (epipf_group.hip): W lanes per particle, launched as grid (B, chains) x 64 W threads
+using GroupStepFn = void (*)(const StepArgs& a, int p, dim3 grid, size_t lds, hipStream_t s);
+GroupStepFn group_step_launcher(int model, int G, int obs, int W, int K);
+bool group_shape_supported(int W, int K);
+size_t group_lds_bytes(int B, int C);
 int prefix_segment(int B);
 constexpr int kMaxSegments = 200;
 hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, const FilterStreams& fs);

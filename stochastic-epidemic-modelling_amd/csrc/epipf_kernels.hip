@@ -11,7 +11,7 @@
 // so the weights, the in-block CDF and the block sums of step p are produced by the same lanes that
 // produced the states, and the next launch only reads them.  The init kernel draws the Poisson initial
 // states (pmcmc.py:156-175) and the first weights.
-#include "epipf_device.hpp"
+#include "epipf_step.hpp"
 #include <algorithm>
 
 #include "epipf_internal.hpp"
@@ -21,60 +21,6 @@
 #endif
 
 namespace epipf {
-
-// exclusive prefix of the B block sums into LDS (bpex), deterministic order; returns the total.
-template <int WG>
-__device__ __forceinline__ double scan_block_sums(const double* __restrict__ bsum_g, int B, double* bpex,
-                                                  double* bsum, double* red) {
-    const int tid = threadIdx.x;
-    const int per = (B + WG - 1) / WG;
-    const int beg = min(tid * per, B), end = min(beg + per, B);
-    double s = 0.0;
-    for (int i = beg; i < end; ++i) {
-        const double v = bsum_g[i];
-        bsum[i] = v;
-        s = s + v;
-    }
-    const double incl = block_inclusive_scan<WG>(s, red);
-    // exclusive offset of this thread's chunk = inclusive result of the previous thread
-    double* incl_lds = bpex + B;  // scratch after bpex (allocated B + WG)
-    incl_lds[tid] = incl;
-    __syncthreads();
-    double e = (tid == 0) ? 0.0 : incl_lds[tid - 1];
-    for (int i = beg; i < end; ++i) {
-        bpex[i] = e;
-        e = e + bsum[i];
-    }
-    __syncthreads();
-    return bpex[B - 1] + bsum[B - 1];
-}
-
-// Segmented prefix of the B block sums (64-thread block): lane l sums the blocks of segments [l*q, (l+1)*q)
-// sequentially, a wave scan gives each lane its offset, and the lane writes seg_start[k] / seg_end[k] (the running
-// sum before / after segment k's S blocks) to LDS.  With S = 1 this is scan_block_sums<64> exactly (seg_start =
-// bpex, seg_end = bpex + bsum).  LDS holds 2 * nseg <= 400 doubles whatever N is, so one-wave blocks keep 7 waves
-// per SIMD at every size (before, past ~16k particles the 2B-double table capped occupancy and 256-thread blocks
-// were needed, whose four waves retire together).
-__device__ __forceinline__ double scan_segments(const double* __restrict__ bsum_g, int B, int S, int nseg,
-                                                double* seg_start, double* seg_end) {
-    const int lane = threadIdx.x;
-    const int q = (nseg + 63) / 64;
-    const int k0 = min(lane * q, nseg), k1 = min(k0 + q, nseg);
-    const int b0 = min(k0 * S, B), b1 = min(k1 * S, B);
-    double s = 0.0;
-    for (int i = b0; i < b1; ++i) s = s + bsum_g[i];
-    const double inc = block_inclusive_scan<64>(s, nullptr);
-    const double up = __shfl_up(inc, 1, 64);
-    double e = (lane == 0) ? 0.0 : up;
-    for (int k = k0; k < k1; ++k) {
-        seg_start[k] = e;
-        const int ie = min((k + 1) * S, B);
-        for (int i = k * S; i < ie; ++i) e = e + bsum_g[i];
-        seg_end[k] = e;
-    }
-    __syncthreads();
-    return seg_end[nseg - 1];
-}
 
 template <int MODEL, int G, int OBS, int WG>
 __global__ __launch_bounds__(WG) void pf_init_kernel(StepArgs a) {
@@ -406,10 +352,15 @@ static size_t resample_lds_bytes(int B, int wg) {
 
 template <int MODEL, int G, int OBS, int WG>
 static hipError_t launch_filter_t(const StepArgs& a, int n_chains, const FilterStreams& fs) {
+    constexpr int C = Shape<MODEL, G>::C;
     // Chains are independent, so chain groups advance through their T steps on separate streams: one group's
     // end-of-launch tail (the last, partial round of waves) overlaps the other groups' launches.
     const size_t lds = step_lds_bytes(a.B, WG);
     const int S = std::max(1, std::min(fs.n, n_chains));
+    // W lanes per particle (runs too small to fill the chip): the lane-group step kernel, epipf_group.hip
+    const GroupStepFn group = a.lanes > 1 ? group_step_launcher(MODEL, G, OBS, a.lanes, a.lane_events) : nullptr;
+    if (a.lanes > 1 && !group) return hipErrorInvalidValue;
+    const size_t glds = group ? group_lds_bytes(a.B, C) : 0;
     for (int g = 0; g < S; ++g) {
         StepArgs ag = a;
         ag.chain0 = (int)((long)n_chains * g / S);
@@ -420,8 +371,10 @@ static hipError_t launch_filter_t(const StepArgs& a, int n_chains, const FilterS
         hipLaunchKernelGGL((pf_init_kernel<MODEL, G, OBS, WG>), grid, block, lds, s, ag);
         if (g == 0 && fs.ev_step0) (void)hipEventRecord(fs.ev_step0, s);
         if (fs.g_begin[g]) (void)hipEventRecord(fs.g_begin[g], s);
-        for (int p = 1; p < a.T; ++p)
-            hipLaunchKernelGGL((pf_step_kernel<MODEL, G, OBS, WG>), grid, block, lds, s, ag, p);
+        for (int p = 1; p < a.T; ++p) {
+            if (group) group(ag, p, grid, glds, s);
+            else hipLaunchKernelGGL((pf_step_kernel<MODEL, G, OBS, WG>), grid, block, lds, s, ag, p);
+        }
         if (fs.g_end[g]) (void)hipEventRecord(fs.g_end[g], s);
         if (g > 0) (void)hipEventRecord(fs.join[g], s);
     }

@@ -1,0 +1,76 @@
+// epipf_step.hpp -- the block-sum prefix helpers shared by the one-lane-per-particle step kernel
+// (epipf_kernels.hip) and the lane-group step kernel (epipf_group.hip).
+#pragma once
+#include "epipf_device.hpp"
+
+namespace epipf {
+
+// LDS ordering between the lanes that run a helper: the whole block (__syncthreads), or only the calling wave
+// (WAVE = true: the lane-group kernel runs these on its first wave while the other waves wait at a block barrier).
+template <bool WAVE>
+__device__ __forceinline__ void lds_sync() {
+    if constexpr (WAVE) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else {
+        __syncthreads();
+    }
+}
+
+// exclusive prefix of the B block sums into LDS (bpex), deterministic order; returns the total.
+template <int WG, bool WAVE = false>
+__device__ __forceinline__ double scan_block_sums(const double* __restrict__ bsum_g, int B, double* bpex,
+                                                  double* bsum, double* red) {
+    const int tid = threadIdx.x;
+    const int per = (B + WG - 1) / WG;
+    const int beg = min(tid * per, B), end = min(beg + per, B);
+    double s = 0.0;
+    for (int i = beg; i < end; ++i) {
+        const double v = bsum_g[i];
+        bsum[i] = v;
+        s = s + v;
+    }
+    const double incl = block_inclusive_scan<WG>(s, red);
+    // exclusive offset of this thread's chunk = inclusive result of the previous thread
+    double* incl_lds = bpex + B;  // scratch after bpex (allocated B + WG)
+    incl_lds[tid] = incl;
+    lds_sync<WAVE>();
+    double e = (tid == 0) ? 0.0 : incl_lds[tid - 1];
+    for (int i = beg; i < end; ++i) {
+        bpex[i] = e;
+        e = e + bsum[i];
+    }
+    lds_sync<WAVE>();
+    return bpex[B - 1] + bsum[B - 1];
+}
+
+// Segmented prefix of the B block sums (64-thread block): lane l sums the blocks of segments [l*q, (l+1)*q)
+// sequentially, a wave scan gives each lane its offset, and the lane writes seg_start[k] / seg_end[k] (the running
+// sum before / after segment k's S blocks) to LDS.  With S = 1 this is scan_block_sums<64> exactly (seg_start =
+// bpex, seg_end = bpex + bsum).  LDS holds 2 * nseg <= 400 doubles whatever N is, so one-wave blocks keep 7 waves
+// per SIMD at every size (before, past ~16k particles the 2B-double table capped occupancy and 256-thread blocks
+// were needed, whose four waves retire together).
+template <bool WAVE = false>
+__device__ __forceinline__ double scan_segments(const double* __restrict__ bsum_g, int B, int S, int nseg,
+                                                double* seg_start, double* seg_end) {
+    const int lane = threadIdx.x;
+    const int q = (nseg + 63) / 64;
+    const int k0 = min(lane * q, nseg), k1 = min(k0 + q, nseg);
+    const int b0 = min(k0 * S, B), b1 = min(k1 * S, B);
+    double s = 0.0;
+    for (int i = b0; i < b1; ++i) s = s + bsum_g[i];
+    const double inc = block_inclusive_scan<64>(s, nullptr);
+    const double up = __shfl_up(inc, 1, 64);
+    double e = (lane == 0) ? 0.0 : up;
+    for (int k = k0; k < k1; ++k) {
+        seg_start[k] = e;
+        const int ie = min((k + 1) * S, B);
+        for (int i = k * S; i < ie; ++i) e = e + bsum_g[i];
+        seg_end[k] = e;
+    }
+    lds_sync<WAVE>();
+    return seg_end[nseg - 1];
+}
+
+}  // namespace epipf

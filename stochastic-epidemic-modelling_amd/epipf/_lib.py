@@ -16,12 +16,12 @@ SIR, SEIR, SIR_SUBGROUPS, SIR_SUBGROUPS2 = 0, 1, 2, 3
 OBS_BINOMIAL, OBS_NORMAL = 0, 1
 RESAMPLE_MULTINOMIAL, RESAMPLE_SYSTEMATIC = 0, 1
 PROFILE_OFF, PROFILE_TIMING, PROFILE_COUNTERS = 0, 1, 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 EXPORTS = (
     "epipf_create", "epipf_destroy", "epipf_set_observations", "epipf_set_population", "epipf_run",
     "epipf_copy_history", "epipf_path_sample", "epipf_simulate", "epipf_resample", "epipf_set_profiling",
-    "epipf_get_stats", "epipf_reset_stats", "epipf_set_streams", "epipf_last_error", "epipf_abi_version", "epipf_device_count",
+    "epipf_get_stats", "epipf_reset_stats", "epipf_set_streams", "epipf_set_lanes", "epipf_last_error", "epipf_abi_version", "epipf_device_count",
     "epipf_abc", "epipf_abc_trials", "epipf_glibc_log", "epipf_simulate_path",
 )
 
@@ -45,6 +45,8 @@ class Stats(ctypes.Structure):
         ("ssa_exact_waves", ctypes.c_int64),
         ("step_kernel_ms", ctypes.c_double),
         ("step_kernel_launches", ctypes.c_int64),
+        ("last_lanes", ctypes.c_int64),
+        ("last_lane_events", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -81,6 +83,7 @@ def load():
         "epipf_resample": ([P, i32, P, P, P, P], i32),
         "epipf_set_profiling": ([P, i32], i32),
         "epipf_set_streams": ([P, i32], i32),
+        "epipf_set_lanes": ([P, i32, i32], i32),
         "epipf_get_stats": ([P, ctypes.POINTER(Stats)], i32),
         "epipf_reset_stats": ([P], i32),
         "epipf_last_error": ([], ctypes.c_char_p),

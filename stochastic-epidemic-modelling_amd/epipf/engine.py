@@ -224,6 +224,11 @@ class Engine:
         """Concurrent chain-group streams used by run() (1..8)."""
         check(self._L.epipf_set_streams(self._h, int(n)), "epipf_set_streams")
 
+    def set_lanes(self, w, events_per_lane=0):
+        """SSA lanes per particle used by run(): 0 = automatic, 1 (one-lane kernel), 2, 4, 8, 16 (lane groups), and
+        the events each lane of a group draws per chunk (0 = automatic)."""
+        check(self._L.epipf_set_lanes(self._h, int(w), int(events_per_lane)), "epipf_set_lanes")
+
     def stats(self):
         s = _lib.Stats()
         check(self._L.epipf_get_stats(self._h, ctypes.byref(s)), "epipf_get_stats")

@@ -1,0 +1,176 @@
+"""The lane-group step kernel (epipf_group.hip: W = 2, 4, 8, 16 lanes per particle, the latency mode for runs that
+do not fill the chip) against the CPU oracle and against the one-lane kernel (W = 1): states and ancestors bit-exact,
+log-likelihoods within 1e-9 absolute, for every model, both observation types, extinct starts, the segmented
+block prefix, the exact-loop branch (EPIPF_SSA_FAST=0) and the full BASELINE config-2 and config-5 sizes at one
+chain.  Needs an MI355X: `-m gpu`."""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+LANES = [1, 2, 4, 8, 16]
+SHAPES = [(2, 1), (4, 1), (8, 1), (16, 1)]   # (W, K) instantiated
+
+
+def _case(datasets_golden, model):
+    if model == "sir":
+        return dict(Y=datasets_golden["sir_binom"][:30], theta=(2.0, 1.0), obs=False, probs=0.1, npop=4820, mu=20, G=1)
+    if model == "sir_normal":
+        return dict(Y=datasets_golden["sir_noisy"][:30], theta=(2.1, 0.9), obs=True, probs=0.5, npop=4820, mu=20, G=1,
+                    model="sir")
+    if model == "seir":
+        return dict(Y=datasets_golden["seir_binom"][:30], theta=(4.0, 1.0, 1.0), obs=False, probs=0.1, npop=4820, mu=20,
+                    G=1)
+    if model in ("sir_subgroups", "sir_subgroups2"):
+        Y = datasets_golden["sub_binom" if model == "sir_subgroups" else "sub2_binom"][:8]
+        return dict(Y=Y, theta=(np.array([[5.0, 2.0], [1.0, 3.0]]), 0.5), obs=False, probs=0.1,
+                    npop=np.array([2030.0, 3040.0]), mu=np.array([30.0, 40.0]), G=2)
+    raise ValueError(model)
+
+
+def _run(model, c, N, chains, lanes, keys, fidx, events=0):
+    from epipf.engine import Engine, model_id, theta_vector
+    mid = model_id(model)
+    th, G = theta_vector(mid, c["theta"])
+    eng = Engine(model, G, N, c["Y"].shape[0], chains)
+    eng.set_observations(c["Y"])
+    eng.set_population(c["npop"], c["mu"])
+    eng.set_lanes(lanes, events)
+    lz, st = eng.run(np.repeat(th[None], chains, 0), [c["probs"]] * chains, keys, fidx, observations=c["obs"])
+    used = eng.stats()["last_lanes"]
+    hid, anc = eng.history(chains)
+    eng.close()
+    return lz, st, hid, anc, used
+
+
+@pytest.mark.parametrize("lanes", LANES)
+@pytest.mark.parametrize("model", ["sir", "sir_normal", "seir", "sir_subgroups", "sir_subgroups2"])
+def test_lane_groups_match_oracle(datasets_golden, model, lanes):
+    c = _case(datasets_golden, model)
+    name = c.get("model", model)
+    N, chains = 700, 2
+    keys, fidx = [31, 32], [4, 9]
+    lz, st, hid, anc, used = _run(name, c, N, chains, lanes, keys, fidx)
+    assert used == lanes
+    for ch in range(chains):
+        o = oracle.particle_filter(c["Y"], name, c["theta"], c["obs"], c["probs"], N, c["npop"], c["mu"],
+                                   key=keys[ch], filter_index=fidx[ch])
+        assert int(st[ch]) == o["status"] == 0
+        np.testing.assert_array_equal(hid[ch], o["hidden"])
+        np.testing.assert_array_equal(anc[ch], o["ancestry"])
+        np.testing.assert_allclose(lz[ch], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("model", ["sir", "seir", "sir_subgroups"])
+def test_every_lane_shape_matches_oracle(datasets_golden, model, shape):
+    """Every instantiated (lanes, events per lane) shape, one chain, against the oracle."""
+    c = _case(datasets_golden, model)
+    W, K = shape
+    lz, st, hid, anc, used = _run(model, c, 400, 1, W, [8], [6], events=K)
+    assert used == W
+    o = oracle.particle_filter(c["Y"], model, c["theta"], c["obs"], c["probs"], 400, c["npop"], c["mu"], key=8,
+                               filter_index=6)
+    assert int(st[0]) == o["status"] == 0
+    np.testing.assert_array_equal(hid[0], o["hidden"])
+    np.testing.assert_array_equal(anc[0], o["ancestry"])
+    np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("G", [3, 4])
+def test_lane_groups_larger_subgroup_models_equal_one_lane(datasets_golden, G):
+    """G = 3, 4 (12 and 20 channels, the widest unrolled decision passes): every W equals W = 1."""
+    rs = np.random.RandomState(G)
+    beta = rs.uniform(0.5, 3.0, (G, G))
+    c = dict(Y=np.tile(datasets_golden["sub_binom"][:6, :3], (1, G)), theta=(beta, 0.7), obs=False, probs=0.1,
+             npop=np.full(G, 1500.0), mu=np.full(G, 15.0), G=G)
+    ref = _run("sir_subgroups", c, 300, 1, 1, [5], [2])
+    for lanes in LANES[1:]:
+        got = _run("sir_subgroups", c, 300, 1, lanes, [5], [2])
+        assert got[4] == lanes
+        assert int(got[1][0]) == int(ref[1][0])
+        np.testing.assert_array_equal(got[2], ref[2])
+        np.testing.assert_array_equal(got[3], ref[3])
+        np.testing.assert_array_equal(got[0], ref[0])
+
+
+@pytest.mark.parametrize("lanes", [2, 16])
+def test_lane_groups_extinct_starts_and_short_horizons(datasets_golden, lanes):
+    """Populations that die out inside a chunk of W events (mu = 1: many particles start with one infected) and
+    T = 2: the group's extinction and step-boundary exits."""
+    Y = datasets_golden["sir_binom"][:2]
+    c = dict(Y=Y, theta=(1.2, 1.0), obs=False, probs=0.1, npop=4820, mu=1.0, G=1)
+    lz, st, hid, anc, _ = _run("sir", c, 333, 1, lanes, [17], [0])
+    o = oracle.particle_filter(Y, "sir", (1.2, 1.0), False, 0.1, 333, 4820, 1.0, key=17, filter_index=0)
+    assert int(st[0]) == o["status"]
+    if o["status"] == 0:
+        np.testing.assert_array_equal(hid[0], o["hidden"])
+        np.testing.assert_array_equal(anc[0], o["ancestry"])
+
+
+def test_lane_groups_exact_loop_branch(datasets_golden, monkeypatch):
+    """EPIPF_SSA_FAST=0: no particle may take the f32 channel test, so every group runs the exact loop branch."""
+    monkeypatch.setenv("EPIPF_SSA_FAST", "0")
+    c = _case(datasets_golden, "seir")
+    lz, st, hid, anc, used = _run("seir", c, 500, 1, 8, [3], [1])
+    assert used == 8
+    o = oracle.particle_filter(c["Y"], "seir", c["theta"], False, 0.1, 500, 4820, 20, key=3, filter_index=1)
+    np.testing.assert_array_equal(hid[0], o["hidden"])
+    np.testing.assert_array_equal(anc[0], o["ancestry"])
+
+
+def test_lane_groups_segmented_prefix(datasets_golden):
+    """N = 12865 (202 blocks: a segmented block-sum prefix) through W = 8 and 16."""
+    Y = datasets_golden["sir_binom"][:4]
+    c = dict(Y=Y, theta=(2.0, 1.0), obs=False, probs=0.1, npop=4820, mu=20, G=1)
+    o = oracle.particle_filter(Y, "sir", (2.0, 1.0), False, 0.1, 12865, 4820, 20, key=77, filter_index=3)
+    for lanes in (8, 16):
+        lz, st, hid, anc, _ = _run("sir", c, 12865, 1, lanes, [77], [3])
+        np.testing.assert_array_equal(hid[0], o["hidden"])
+        np.testing.assert_array_equal(anc[0], o["ancestry"])
+        np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("cfg", [2, 5])
+def test_lane_groups_full_size_single_chain_vs_oracle(cfg):
+    """BASELINE config 2 (SIR, N = 10^4, T = 200) and config 5 (2-group SIR, N = 10^4) at the north star's layout, one
+    chain per GPU, on the automatic lane choice (W = 4 there): bit-exact vs the oracle."""
+    from epipf import datasets
+    from epipf.engine import Engine, model_id, theta_vector
+    Y, meta = datasets.benchmark_dataset(cfg)
+    mid = model_id(meta["model"])
+    base = np.asarray(meta["theta"], dtype=np.float64)
+    if mid >= 2:
+        G = int(round(np.sqrt(base.size - 1)))
+        ref_th = (base[:G * G].reshape(G, G), base[-1])
+    else:
+        G, ref_th = 1, tuple(base)
+    eng = Engine(meta["model"], G, meta["N"], Y.shape[0], 1)
+    eng.set_observations(Y)
+    eng.set_population(meta["n_population"], meta["mu"])
+    obs = bool(meta.get("observations", False))
+    lz, st = eng.run(theta_vector(mid, ref_th)[0][None], [meta["probs"]], [4242], [7], observations=obs)
+    assert eng.stats()["last_lanes"] == 4
+    hid, anc = eng.history(1)
+    eng.close()
+    o = oracle.particle_filter(Y, meta["model"], ref_th, obs, meta["probs"], meta["N"], meta["n_population"],
+                               meta["mu"], key=4242, filter_index=7)
+    assert int(st[0]) == o["status"] == 0
+    np.testing.assert_array_equal(hid[0], o["hidden"])
+    np.testing.assert_array_equal(anc[0], o["ancestry"])
+    np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
+def test_automatic_lane_choice():
+    """Up to 8 chains of 10^4 particles get 4 lanes; a batch that fills the chip keeps one lane per particle."""
+    from epipf.engine import Engine
+    Y = np.zeros((3, 3))
+    eng = Engine("sir", 1, 10000, 3, 256)
+    eng.set_observations(Y)
+    eng.set_population(10000, 20)
+    for chains, want in [(1, 4), (2, 4), (8, 4), (9, 1), (256, 1)]:
+        eng.run(np.tile([0.25, 0.1], (chains, 1)), [0.1] * chains, list(range(1, chains + 1)), [0] * chains)
+        assert eng.stats()["last_lanes"] == want, (chains, eng.stats()["last_lanes"])
+    eng.close()
