@@ -13,13 +13,16 @@ FILTER_CASES = ["sir_binom", "sir_normal", "seir_binom", "sub_binom", "sub2_bino
                 "cfg3_seir_normal", "sir_theta_off", "degenerate"]
 
 
-def engine_for(a, chains=1):
+def engine_for(a, chains=1, lanes=0):
+    """The cached engine for a case; lanes: SSA lanes per particle (0 = automatic: the lane-group kernel for runs
+    below ~8 chains of 10^4 particles, 1 = the one-lane kernel), set on every call."""
     from epipf.engine import get_engine, model_id, theta_vector
     mid = model_id(a["model"])
     th, G = theta_vector(mid, a["theta"])
     eng = get_engine(mid, G, a["N"], a["Y"].shape[0], chains)
     eng.set_observations(a["Y"])
     eng.set_population(a["npop"], a["mu"])
+    eng.set_lanes(lanes)
     return eng, th
 
 
@@ -40,11 +43,12 @@ def test_filter_matches_reference_golden(filter_golden, name):
     np.testing.assert_allclose(lz[0][ok], np.log(z[ok]), rtol=0, atol=1e-9)
 
 
+@pytest.mark.parametrize("lanes", [0, 1])
 @pytest.mark.parametrize("name", FILTER_CASES)
-def test_filter_matches_oracle(filter_golden, name):
+def test_filter_matches_oracle(filter_golden, name, lanes):
     rec = filter_golden["filter_" + name]
     a = case_args(rec)
-    eng, th = engine_for(a)
+    eng, th = engine_for(a, lanes=lanes)
     lz, st = eng.run(th[None], [a["probs"]], [a["key"]], [a["f"]], observations=a["observations"])
     o = oracle.particle_filter(a["Y"], a["model"], a["theta"], a["observations"], a["probs"], a["N"], a["npop"],
                                a["mu"], key=a["key"], filter_index=a["f"])
@@ -57,8 +61,9 @@ def test_filter_matches_oracle(filter_golden, name):
     np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
 
 
+@pytest.mark.parametrize("lanes", [0, 1])
 @pytest.mark.parametrize("seed", range(6))
-def test_filter_random_configs_vs_oracle(datasets_golden, seed):
+def test_filter_random_configs_vs_oracle(datasets_golden, seed, lanes):
     """Seeded random (theta, N, key) on every model: bit-exact states/ancestors vs the oracle."""
     rs = np.random.RandomState(100 + seed)
     model = ["sir", "seir", "sir_subgroups", "sir_subgroups2", "sir", "seir"][seed]
@@ -77,7 +82,7 @@ def test_filter_random_configs_vs_oracle(datasets_golden, seed):
         N = min(N, 300)
     a = dict(Y=Y, model=model, theta=th, observations=obs, probs=probs, N=N, npop=npop, mu=mu,
              key=int(rs.randint(1, 2**31)), f=int(rs.randint(0, 1000)))
-    eng, thv = engine_for(a)
+    eng, thv = engine_for(a, lanes=lanes)
     lz, st = eng.run(thv[None], [probs], [a["key"]], [a["f"]], observations=obs)
     o = oracle.particle_filter(Y, model, th, obs, probs, N, npop, mu, key=a["key"], filter_index=a["f"])
     assert int(st[0]) == o["status"]
@@ -374,12 +379,13 @@ def test_systematic_resampling_vs_oracle(datasets_golden):
     np.testing.assert_array_equal(hid[0], o["hidden"])
 
 
-def test_full_size_cfg2_properties(datasets_golden):
-    """BASELINE config 2 at full size (N=10,000, T=200): conservation, ancestor range, log-likelihood
-    agreement with the oracle (threaded C) and determinism of the run."""
+@pytest.mark.parametrize("lanes", [1, 0])
+def test_full_size_cfg2_properties(datasets_golden, lanes):
+    """BASELINE config 2 at full size (N=10,000, T=200), one-lane and lane-group kernels: conservation, ancestor
+    range, states / ancestors / log-likelihoods vs the oracle (threaded C)."""
     Y = datasets_golden["cfg2_binom"]
     a = dict(Y=Y, model="sir", theta=(0.25, 0.1), N=10000, npop=10000, mu=20)
-    eng, th = engine_for(a)
+    eng, th = engine_for(a, lanes=lanes)
     lz, st = eng.run(th[None], 0.1, 2024, 0)
     assert st[0] == 0
     hid, anc = eng.history(1)
@@ -393,7 +399,9 @@ def test_full_size_cfg2_properties(datasets_golden):
 
 def _engine_with_fast_ssa(enabled, N, T, chains, model="sir", groups=1, slack=None):
     """A fresh context with the certified f32 event loop on or off (EPIPF_SSA_FAST is read at create), and
-    optionally its clock band widened `slack` times (EPIPF_CLOCK_SLACK: more replays, same results)."""
+    optionally its clock band widened `slack` times (EPIPF_CLOCK_SLACK: more replays, same results).  One lane per
+    particle: these tests are about the one-lane kernel's f32 loop and its replays (the lane-group kernel has its
+    own in tests/test_gpu_lanes.py)."""
     import os
     from epipf.engine import Engine
     env = {"EPIPF_SSA_FAST": "1" if enabled else "0", "EPIPF_CLOCK_SLACK": None if slack is None else str(slack)}
@@ -404,7 +412,9 @@ def _engine_with_fast_ssa(enabled, N, T, chains, model="sir", groups=1, slack=No
         else:
             os.environ[k] = v
     try:
-        return Engine(model, groups, N, T, chains)
+        eng = Engine(model, groups, N, T, chains)
+        eng.set_lanes(1)
+        return eng
     finally:
         for k, v in old.items():
             if v is None:
