@@ -250,7 +250,10 @@ def main():
             pmc = json.load(open(pmc_path))
         except (OSError, ValueError):
             pmc = {}
-    if pmc.get("config", 2) == args.config and pmc.get("chains_per_gpu", C) == C:
+    # SSA lanes per particle of the timed runs (1: pf_step_kernel; > 1: the lane-group kernel)
+    lanes = int(engines[0].stats()["last_lanes"]) or 1
+    # the committed PMC pass profiles the default bench (config 2, 256 chains per GPU, one lane per particle)
+    if pmc.get("config", 2) == args.config and pmc.get("chains_per_gpu", 256) == C and lanes == 1:
         # MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE counts half the bytes of a coalesced read stream, so
         # `traffic` doubles the read side (FETCH x 2 + WRITE); the raw counter sum is `traffic_raw`
         per_unit = pmc.get("hbm_bytes_per_particle_step_read_doubled")
@@ -350,7 +353,7 @@ def main():
                                       f"draws at end"},
             # pf_step_kernel is bound by vector-instruction issue (the SSA event loop), not by HBM: the primary
             # roofline is VALU issue; the HBM figures the north star asks for are in `hbm`
-            "roofline": {"bound": "valu", "kernel": "pf_step_kernel",
+            "roofline": {"bound": "valu", "kernel": "pf_step_kernel" if lanes == 1 else f"pf_step_group_kernel (W={lanes})",
                          "achieved": valu["achieved"] if valu else None, "peak": VALU_PEAK,
                          "unit": "wave64 VALU instr/s", "frac": valu["achieved"] / VALU_PEAK if valu else None,
                          "traffic": traffic, "valu_issue": valu, "hbm": hbm,
@@ -361,7 +364,8 @@ def main():
                          # launch waits for CUs held by the concurrent chain-group launches
                          "rocprof_avg_launch_us": rocprof_us},
             "events_per_s": events_per_s,
-            "ssa_lane_utilisation": lane_use,
+            "ssa_lane_utilisation": lane_use if lanes == 1 else None,
+            "lanes_per_particle": lanes,
             "resample_fallbacks": st["resample_fallbacks"],
             "events_per_particle_step": cst["events"] / cst["particle_steps"] if cst["particle_steps"] else None,
             # particle-steps the certified f32 SSA path handed to the exact loop, and waves that waited on one

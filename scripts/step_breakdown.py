@@ -12,19 +12,20 @@ sys.path.insert(0, os.path.join(REPO, "stochastic-epidemic-modelling_amd"))
 from epipf import _lib, datasets  # noqa: E402
 from epipf import pmcmc as pm  # noqa: E402
 
-Y, meta = datasets.benchmark_dataset(2)
+Y, meta = datasets.benchmark_dataset(int(os.environ.get("CFG", 2)))
 C = int(os.environ.get("CHAINS", 256))
-s = pm.ChainSampler(Y, "sir", list(meta["theta"]), 1e-4, iters=12, probs=0.1, n_particles=meta["N"],
+s = pm.ChainSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=12, probs=meta["probs"],
+                    observations=meta.get("observations", False), n_particles=meta["N"],
                     n_population=meta["n_population"], mu=meta["mu"],
                     rngs=[np.random.RandomState(2024 + g) for g in range(C)],
                     keys=[pm.chain_key(2024, g) for g in range(C)], mh_ratio="log")
 tim = {"run": 0.0, "path": 0.0}
-run0, path0 = s._run_batch, s._path_sample
+run0, path0 = s.eng.run, s._path_sample
 
 
-def run_t(props):
+def run_t(*args, **kw):
     t = time.perf_counter()
-    r = run0(props)
+    r = run0(*args, **kw)
     tim["run"] += time.perf_counter() - t
     return r
 
@@ -36,7 +37,7 @@ def path_t(ok):
     return r
 
 
-s._run_batch, s._path_sample = run_t, path_t
+s.eng.run, s._path_sample = run_t, path_t
 s.initialise()
 s.step()
 s.eng.reset_stats()

@@ -225,7 +225,10 @@ class ChainSampler:
         self.thetas = np.zeros((nc, self.iters, d))
         self.likelihoods = np.zeros((nc, self.iters))
         self.loglik = np.zeros((nc, self.iters))
-        self.trajs = np.zeros((nc, T, self.iters, Cc))
+        # sampled trajectories, iteration-major per chain (one contiguous [T, C] block per MH iteration, so an
+        # iteration's bookkeeping is a block copy); `trajs` is the [chains, T, iters, C] view of the reference layout
+        self._tr = np.zeros((nc, self.iters, T, Cc))
+        self.trajs = self._tr.transpose(0, 2, 1, 3)
         S = None if sigma is None else np.asarray(sigma, dtype=np.float64)
         self.std = [np.eye(d) if S is None else (S[c] if S.ndim == 3 else S).copy() for c in range(nc)]
         self._fac = [None] * nc                                  # multivariate_normal factor of h * std[c]
@@ -290,7 +293,7 @@ class ChainSampler:
         self.thetas[c, i] = self.thetas[c, i - 1]
         self.likelihoods[c, i] = self.likelihoods[c, i - 1]
         self.loglik[c, i] = self.loglik[c, i - 1]
-        self.trajs[c, :, i, :] = self.trajs[c, :, i - 1, :]
+        self._tr[c, i] = self._tr[c, i - 1]
 
     def initialise(self):
         """The initial draw loop, pmcmc.py:276-318 (repeat until theta >= 0 and the filter succeeded)."""
@@ -322,52 +325,64 @@ class ChainSampler:
     def step(self):
         """One MH iteration for every chain, pmcmc.py:325-406.  Returns the number of chains that ran a filter.
         Per chain the RNG calls keep the reference's order (proposal normals, path-pick randint, acceptance
-        uniform); the bookkeeping (accepted rows, copies of the previous row) is one array assignment per field."""
+        uniform); everything else -- the negative-proposal test, the batch arrays, the accepted rows and the copies
+        of the previous row -- is one array operation over the chains."""
         i = self.i
-        props = {}
-        for c in range(self.nc):
+        nc, d = self.nc, self.d
+        P = np.empty((nc, d))
+        for c in range(nc):
             if self.adaptive and i > 1e3:
                 self.std[c] = np.cov(self.thetas[c, :i].T, ddof=0) + 1e-4 * np.eye(self.d)
                 self._fac[c] = None
-            prop = self._propose(c, self.thetas[c, i - 1])
-            if (prop < 0).any():                                  # sum(prop < 0) > 0, pmcmc.py:333-337
-                continue
-            props[c] = prop
-        acc = []
-        if props:
-            lz, st, stripped = self._run_batch(props)
-            ok = [c for c in props if st[c] == _lib.STATUS_OK]     # degenerate filters: rejected, :365-369
-            tr = self._path_sample(ok) if ok else None
-            new_th = []
-            for c in ok:
-                th, p2 = stripped[c]
-                theta_new = np.append(th, p2) if self.probs is None else props[c]
-                if self.mh_ratio == "reference":
-                    prob = _reference_ratio(np.exp(lz[c, -1]), self.likelihoods[c, i - 1], theta_new,
-                                            self.thetas[c, i - 1], self.params[c], self.h * self.std[c])
-                else:
-                    prob = _log_ratio(lz[c, -1], self.loglik[c, i - 1])
-                if self.rngs[c].random_sample() < prob:            # == uniform(): 0 + 1*U, 7x cheaper
-                    acc.append(c)
-                    new_th.append(theta_new)
-            if acc:
-                a = np.asarray(acc)
-                self.thetas[a, i] = np.asarray(new_th)
-                self.loglik[a, i] = lz[a, -1]
-                self.likelihoods[a, i] = np.exp(lz[a, -1])
-                self.trajs[a, :, i, :] = tr[a]
-                for c in acc:
-                    self.acceptances[c] += 1
-        rej = np.ones(self.nc, dtype=bool)
+            P[c] = self._propose(c, self.thetas[c, i - 1])
+        live = ~(P < 0).any(axis=1)                               # sum(prop < 0) > 0: no filter, :333-337
+        lv = np.flatnonzero(live)
+        acc = np.zeros(0, dtype=np.intp)
+        if lv.size:
+            if self.probs is None:                                # pmcmc.py:339-346: the last entry is probs
+                th_all, pr_all = P[:, :-1], np.clip(P[:, -1], 0.0, 1.0)
+                new_all = np.concatenate([th_all, pr_all[:, None]], axis=1)
+            else:
+                th_all, pr_all, new_all = P, np.full(nc, float(self.probs)), P
+            fidx = np.zeros(nc, dtype=np.uint64)
+            for c in lv.tolist():
+                fidx[c] = self.fnext[c]
+                self.fnext[c] += 1
+                self.filters_run[c] += 1
+            self._bind()
+            lz, st = self.eng.run(np.ascontiguousarray(th_all), pr_all, self.keys, fidx,
+                                  observations=self.observations, active=live.astype(np.int32), resample=self.resample)
+            self.last_active = int(lv.size)
+            ok = np.flatnonzero(live & (st == _lib.STATUS_OK))    # degenerate filters: rejected, :365-369
+            if ok.size:
+                tr = self._path_sample(ok.tolist())
+                lzT = lz[:, -1]
+                take = []
+                for c in ok.tolist():
+                    if self.mh_ratio == "reference":
+                        prob = _reference_ratio(np.exp(lzT[c]), self.likelihoods[c, i - 1], new_all[c],
+                                                self.thetas[c, i - 1], self.params[c], self.h * self.std[c])
+                    else:
+                        prob = _log_ratio(lzT[c], self.loglik[c, i - 1])
+                    if self.rngs[c].random_sample() < prob:        # == uniform(): 0 + 1*U, 7x cheaper
+                        take.append(c)
+                        self.acceptances[c] += 1
+                if take:
+                    acc = np.asarray(take, dtype=np.intp)
+                    self.thetas[acc, i] = new_all[acc]
+                    self.loglik[acc, i] = lzT[acc]
+                    self.likelihoods[acc, i] = np.exp(lzT[acc])
+                    self._tr[acc, i] = tr[acc]
+        rej = np.ones(nc, dtype=bool)
         rej[acc] = False
         if rej.any():                                             # rejected, negative or degenerate: previous row
             r = np.flatnonzero(rej)
             self.thetas[r, i] = self.thetas[r, i - 1]
             self.likelihoods[r, i] = self.likelihoods[r, i - 1]
             self.loglik[r, i] = self.loglik[r, i - 1]
-            self.trajs[r, :, i, :] = self.trajs[r, :, i - 1, :]
+            self._tr[r, i] = self._tr[r, i - 1]
         self.i += 1
-        return len(props)
+        return int(lv.size)
 
     def run(self, progress=False, on_iteration=None):
         if self.i == 0:
