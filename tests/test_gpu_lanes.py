@@ -133,10 +133,11 @@ def test_lane_groups_segmented_prefix(datasets_golden):
         np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
 
 
-@pytest.mark.parametrize("cfg", [2, 5])
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_lane_groups_full_size_single_chain_vs_oracle(cfg):
-    """BASELINE config 2 (SIR, N = 10^4, T = 200) and config 5 (2-group SIR, N = 10^4) at the north star's layout, one
-    chain per GPU, on the automatic lane choice (W = 4 there): bit-exact vs the oracle."""
+    """Every BASELINE config at full size with one chain (the north star's layout for config 5), on the automatic
+    lane choice (W = 4 there): config 2 (SIR, N = 10^4, T = 200), 3 (SEIR, normal observations), 4 (N = 5*10^4: 782
+    particle blocks, a segmented block-sum prefix), 5 (2-group SIR) -- bit-exact vs the oracle."""
     from epipf import datasets
     from epipf.engine import Engine, model_id, theta_vector
     Y, meta = datasets.benchmark_dataset(cfg)
