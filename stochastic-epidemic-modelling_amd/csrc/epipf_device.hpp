@@ -542,11 +542,22 @@ struct FastSubgroups {                                                 // gilles
     }
     // Channel ch = g*(G+1) + c: c < G is infection s_{g}_{c} (S[c] -> I[c], :183), c = G recovery i_{g} (I[g] -> R,
     // :185).  Only one group moves, q = c or g: a per-group select instead of a branch per channel (the compiler
-    // turns the channel-by-channel form into a divergent switch).
+    // turns the channel-by-channel form into a divergent switch).  Whether ch is an infection and the group q it
+    // moves are bit fields of compile-time masks (one bit-field extract each, no division by G + 1).
+    static constexpr uint32_t chan_mask(int what) {      // what = -1: infection bits; 0/1: bit `what` of q
+        uint32_t m = 0;
+        for (int ch = 0; ch < NCH; ++ch) {
+            const int g = ch / (G + 1), c = ch % (G + 1), q = c < G ? c : g;
+            const bool bit = what < 0 ? c < G : ((q >> what) & 1) != 0;
+            m |= bit ? (1u << ch) : 0u;
+        }
+        return m;
+    }
+    static constexpr uint32_t kInfMask = chan_mask(-1), kQ0 = chan_mask(0), kQ1 = chan_mask(1);
     __device__ __forceinline__ void apply(int ch, float s) {
-        const int g = ch / (G + 1), c = ch - g * (G + 1);
-        const bool inf = c < G;
-        const int q = inf ? c : g;
+        static_assert(NCH <= 32 && G <= 4, "channel masks");
+        const bool inf = ((kInfMask >> ch) & 1u) != 0u;
+        const int q = (int)((kQ0 >> ch) & 1u) | (G > 2 ? (int)(((kQ1 >> ch) & 1u) << 1) : 0);
         const float dS = inf ? s : 0.f, dI = inf ? s : -s;
 #pragma unroll
         for (int r = 0; r < G; ++r) {

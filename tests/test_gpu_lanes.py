@@ -175,3 +175,32 @@ def test_automatic_lane_choice():
         eng.run(np.tile([0.25, 0.1], (chains, 1)), [0.1] * chains, list(range(1, chains + 1)), [0] * chains)
         assert eng.stats()["last_lanes"] == want, (chains, eng.stats()["last_lanes"])
     eng.close()
+
+
+@pytest.mark.parametrize("lanes", [1, 4])
+def test_populations_past_the_f32_range_take_the_exact_loop(lanes):
+    """A population of 2*10^7 (> 2^24: counts no longer exact in f32) makes every particle ineligible for the certified
+    f32 loop, so both kernels run the exact f64 event loop (the one-lane kernel per lane, the lane-group kernel per
+    group): bit-exact vs the oracle, and the f32 loop is not used (no replays counted)."""
+    from epipf import _lib
+    npop, T, N = 2.0e7, 6, 256
+    Y = np.stack([np.full(T, 0.1 * (npop - 40.0)), 0.1 * np.array([20., 40., 80., 150., 300., 600.]),
+                  np.floor(0.1 * np.array([0., 10., 30., 70., 150., 300.]))], axis=1).astype(np.float64)
+    Y = np.floor(Y)
+    c = dict(Y=Y, theta=(1.6, 0.9), obs=False, probs=0.1, npop=npop, mu=20.0, G=1)
+    from epipf.engine import Engine
+    eng = Engine("sir", 1, N, T, 1)
+    eng.set_observations(Y)
+    eng.set_population(npop, 20.0)
+    eng.set_lanes(lanes)
+    eng.set_profiling(_lib.PROFILE_COUNTERS)
+    lz, st = eng.run(np.array([[1.6, 0.9]]), [0.1], [12], [3])
+    stats = eng.stats()
+    hid, anc = eng.history(1)
+    eng.close()
+    o = oracle.particle_filter(Y, "sir", (1.6, 0.9), False, 0.1, N, npop, 20.0, key=12, filter_index=3)
+    assert int(st[0]) == o["status"] == 0
+    assert stats["last_lanes"] == lanes and stats["events"] > 0
+    np.testing.assert_array_equal(hid[0], o["hidden"])
+    np.testing.assert_array_equal(anc[0], o["ancestry"])
+    np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
