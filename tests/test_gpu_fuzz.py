@@ -1,0 +1,96 @@
+"""Randomised parity sweep of the HIP filter against the CPU oracle: 96 seeded cases over every model (SIR, SEIR, the
+G = 1..4 subgroup model, the group-summed model G = 1..3), both observation types where the reference defines them,
+multinomial and systematic resampling, N from 1 to 3000 (ragged blocks), T from 1 to 12, populations from tens to
+10^6, extinct starts (mu = 0), 1-3 chains per launch with their own keys and filter indices, and every SSA lane count
+(automatic, 1, 2, 4, 8, 16).  Observations are drawn around the ODE-free "probs x initial state" scale so that most
+filters run to the end and some degenerate; the status, every state and every ancestor must equal the oracle's and the
+log-likelihoods agree within 1e-9.  Needs an MI355X: `-m gpu`."""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+CASES = 96
+
+
+def _case(seed):
+    rs = np.random.RandomState(7000 + seed)
+    model = ["sir", "seir", "sir_subgroups", "sir_subgroups2"][seed % 4]
+    G = 1 if model in ("sir", "seir") else int(rs.randint(1, 5 if model == "sir_subgroups" else 4))
+    C = 3 if model == "sir" else 4 if model == "seir" else 3 * G
+    K = 3 if model == "sir_subgroups2" else C
+    obs = bool(rs.rand() < 0.3) and model in ("sir", "seir")
+    N = int(rs.choice([1, 2, 63, 64, 65, 127, 300, 1000, 3000]))
+    T = int(rs.randint(1, 13))
+    npop = np.round(rs.choice([60.0, 500.0, 4820.0, 2e4, 1e6], size=G)).astype(np.float64)
+    mu = np.where(rs.rand(G) < 0.1, 0.0, np.round(rs.uniform(1, 40, G)))
+    mu = np.minimum(mu, npop / 2)
+    probs = float(rs.choice([0.1, 0.3, 0.5])) if obs else float(rs.choice([0.05, 0.1, 0.4]))
+    if model == "sir":
+        theta = tuple(rs.uniform(0.2, 3.0, 2))
+    elif model == "seir":
+        theta = tuple(rs.uniform(0.2, 3.0, 3))
+    else:
+        theta = (rs.uniform(0.2, 4.0, (G, G)), float(rs.uniform(0.2, 1.5)))
+    # observations around probs x the initial compartments, growing a little with t
+    base = np.zeros(C)
+    for g in range(G):
+        if model == "seir":
+            base[:] = [npop[0] - mu[0], 0.0, mu[0], 0.0]
+        else:
+            base[3 * g:3 * g + 3] = [npop[g] - mu[g], mu[g], 0.0]
+    Y = np.zeros((T, K))
+    for t in range(T):
+        x = base.copy()
+        shift = min(t * 3.0, x[0])
+        if model == "seir":
+            x[0] -= shift; x[1] += shift / 3; x[2] += shift / 3; x[3] += shift / 3
+        else:
+            for g in range(G):
+                s = min(t * 3.0, x[3 * g])
+                x[3 * g] -= s; x[3 * g + 1] += s / 2; x[3 * g + 2] += s / 2
+        xo = x if model != "sir_subgroups2" else x.reshape(G, 3).sum(0)
+        Y[t] = np.floor(probs * xo) if not obs else np.floor(xo * (1 + 0.05 * rs.standard_normal(K)))
+    chains = int(rs.randint(1, 4))
+    lanes = int(rs.choice([0, 1, 2, 4, 8, 16]))
+    resample = "systematic" if rs.rand() < 0.25 else "multinomial"
+    keys = [int(k) for k in rs.randint(1, 2**31, chains)]
+    fidx = [int(f) for f in rs.randint(0, 10**6, chains)]
+    thetas = []
+    for c in range(chains):                              # chain c: the case's theta scaled a little
+        if model in ("sir", "seir"):
+            thetas.append(tuple(np.asarray(theta) * (1 + 0.05 * c)))
+        else:
+            thetas.append((theta[0] * (1 + 0.05 * c), theta[1]))
+    return dict(model=model, G=G, obs=obs, N=N, Y=Y, npop=npop, mu=mu, probs=probs, thetas=thetas, keys=keys,
+                fidx=fidx, lanes=lanes, resample=resample)
+
+
+@pytest.mark.parametrize("seed", range(CASES))
+def test_random_filters_match_oracle(seed):
+    from epipf.engine import Engine, model_id, theta_vector
+    a = _case(seed)
+    mid = model_id(a["model"])
+    th = np.stack([theta_vector(mid, t)[0] for t in a["thetas"]])
+    chains = th.shape[0]
+    eng = Engine(a["model"], a["G"], a["N"], a["Y"].shape[0], chains)
+    eng.set_observations(a["Y"])
+    eng.set_population(a["npop"], a["mu"])
+    eng.set_lanes(a["lanes"])
+    lz, st = eng.run(th, [a["probs"]] * chains, a["keys"], a["fidx"], observations=a["obs"], resample=a["resample"])
+    hid, anc = eng.history(chains)
+    eng.close()
+    for c in range(chains):
+        o = oracle.particle_filter(a["Y"], a["model"], a["thetas"][c], a["obs"], a["probs"], a["N"], a["npop"],
+                                   a["mu"], key=a["keys"][c], filter_index=a["fidx"][c], resample=a["resample"])
+        assert int(st[c]) == o["status"], (seed, c, a["model"], a["G"], a["N"], int(st[c]), o["status"])
+        # a degenerate filter (all weights 0 / NaN at some step: the reference's ValueError) is compared up to the
+        # step that failed, where both report -inf
+        olz = o["log_zetas"]
+        P = len(olz) if not o["status"] else int(np.argmax(~np.isfinite(olz)))
+        assert not o["status"] or not np.isfinite(lz[c, P]), (seed, c, lz[c, P])
+        np.testing.assert_array_equal(hid[c][:P], o["hidden"][:P], err_msg=f"seed {seed} chain {c}")
+        np.testing.assert_array_equal(anc[c][:P], o["ancestry"][:P], err_msg=f"seed {seed} chain {c}")
+        np.testing.assert_allclose(lz[c][:P], olz[:P], rtol=1e-12, atol=1e-9, err_msg=f"seed {seed} chain {c}")
