@@ -132,7 +132,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("EPIPF_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI; gloo only for rehearsals
     dist = None
-    if world > 1:
+    # EPIPF_BENCH_DIST=1: the distributed path (process group, max/sum reductions, RCCL all-gather) even at one rank,
+    # so that a one-GPU box rehearses the RCCL code of the driver's N-GPU runs (scripts/rccl_bench_check.sh)
+    force_dist = os.environ.get("EPIPF_BENCH_DIST") == "1"
+    if world > 1 or force_dist:
         import torch
         import torch.distributed as dist
         ndev = torch.cuda.device_count()
@@ -195,7 +198,7 @@ def main():
         filters = sum(samplers[0].step() for _ in range(args.steps))
     # end of run: gather every rank's posterior draws over RCCL (xGMI), SURVEY.md §8e
     results = [r for s_ in samplers for r in s_.results()]
-    gathered = gather_draws(pack_draws(results, upto=samplers[0].i), local)
+    gathered = gather_draws(pack_draws(results, upto=samplers[0].i), local, force=force_dist)
     barrier()
     dt = time.perf_counter() - t0
     st = stats_sum()
