@@ -99,6 +99,7 @@ struct epipf_ctx {
     int lanes = 0;           // SSA lanes per particle: 0 = automatic (pick_lanes), else 1/2/4/8/16 (EPIPF_LANES)
     int lane_events = 0;     // events per lane per chunk of the lane-group kernel: 0 = automatic (EPIPF_LANE_EVENTS)
     int lane_blocks = 1280;  // automatic choice: lane groups up to this many particle blocks per launch
+    int xcd_map = 1;         // XCD-aware placement of the step launches' blocks (EPIPF_XCD_MAP=0: 2-D grid)
 };
 
 // Lanes per particle for a run of n_chains filters.  The one-lane kernel needs ~20k waves per launch to fill the
@@ -205,6 +206,7 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     }
     if (const char* e = getenv("EPIPF_LANE_BLOCKS")) c->lane_blocks = std::max(0, atoi(e));
     if (const char* e = getenv("EPIPF_LANE_EVENTS")) c->lane_events = std::max(0, atoi(e));
+    if (const char* e = getenv("EPIPF_XCD_MAP")) c->xcd_map = atoi(e) != 0;
     c->B = (n_particles + c->wg - 1) / c->wg;
     if (step_lds_bytes(c->B, c->wg) > 160 * 1024) {
         free_ctx(c);
@@ -357,6 +359,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     a.counters = c->counters;
     a.lanes = pick_lanes(c, n_chains);
     a.lane_events = pick_lane_events(c, a.lanes);
+    a.xcd_map = c->xcd_map;
     if (a.lanes > 1 && !group_shape_supported(a.lanes, a.lane_events))
         return fail(EPIPF_EINVAL, "no lane-group kernel for %d lanes x %d events", a.lanes, a.lane_events);
     c->stats.last_lanes = a.lanes;

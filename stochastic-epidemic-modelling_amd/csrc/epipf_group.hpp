@@ -268,7 +268,8 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
     int32_t* rows = reinterpret_cast<int32_t*>(red + 16);
     double* seg_start = red + 16 + (64 * C + 1) / 2;
     double* seg_end = seg_start + a.nseg;
-    const int chain = a.chain0 + (int)blockIdx.y;
+    const BlockPos bp = step_block(a);
+    const int chain = bp.chain;
     const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
     if (a.status[chain] != 0) return;
     const ChainParam cp = a.cp[chain];
@@ -280,13 +281,13 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
     for (int i = (int)threadIdx.x; i < kLogTabEntries; i += 64 * W) tab[i] = a.logtab[i];
 
     if (wave == 0) {                                     // likelihood, resampling, gather: pf_step_kernel's code
-        const int j = (int)blockIdx.x * 64 + lane;
+        const int j = bp.b * 64 + lane;
         const double total = (a.seg == 1)
                                  ? scan_block_sums<64, true>(a.bsum + bprev, a.B, seg_start + a.B, seg_start, red)
                                  : scan_segments<true>(a.bsum + bprev, a.B, a.seg, a.nseg, seg_start, seg_end);
         if (lane == 0) red[0] = total;
         if (total > 0.0) {
-            if (blockIdx.x == 0 && lane == 0)            // pmcmc.py:183, in log space
+            if (bp.b == 0 && lane == 0)            // pmcmc.py:183, in log space
                 a.log_zeta[(size_t)chain * a.T + p] = a.log_zeta[(size_t)chain * a.T + p - 1] + log(total / (double)a.N);
             double U = 0.0;
             int anc = 0;
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
 #pragma unroll
                 for (int c = 0; c < C; ++c) rows[lane * C + c] = hp[c];
             }
-        } else if (blockIdx.x == 0 && lane == 0) {       // all weights 0 or NaN: :187-192
+        } else if (bp.b == 0 && lane == 0) {       // all weights 0 or NaN: :187-192
             a.status[chain] = 1;
             a.log_zeta[(size_t)chain * a.T + p] = -__builtin_inf();
         }
@@ -332,7 +333,7 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
     // group SSA: wave w, group g runs particle w * PPW + g of the block
     const int gl = lane & (W - 1);
     const int pl = wave * PPW + lane / W;
-    const int jg = (int)blockIdx.x * 64 + pl;
+    const int jg = bp.b * 64 + pl;
     int nev = 0;
     double x[C];
     if (jg < a.N) {                                      // group-uniform
@@ -355,7 +356,7 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
     __syncthreads();
 
     if (wave == 0) {                                     // store, weights for step p+1, in-block scan
-        const int j = (int)blockIdx.x * 64 + lane;
+        const int j = bp.b * 64 + lane;
         double w = 0.0;
         if (j < a.N) {
             double xs[C];
@@ -370,7 +371,7 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
             const double loc = block_inclusive_scan<64>(w, red);
             a.wraw[wcur + j] = w;
             a.wloc[wcur + j] = loc;
-            if (lane == 63) a.bsum[bcur + blockIdx.x] = loc;
+            if (lane == 63) a.bsum[bcur + bp.b] = loc;
         }
     }
 }

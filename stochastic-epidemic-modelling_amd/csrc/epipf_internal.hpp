@@ -30,6 +30,7 @@ struct StepArgs {
     int chain0;                   // first chain of this launch (chain groups run on separate streams)
     int lanes;                    // lanes per particle in the SSA: 1 = pf_step_kernel, 2..16 = pf_step_group_kernel
     int lane_events;              // pf_step_group_kernel: events per lane per chunk
+    int xcd_map;                  // 1: 1-D grid of B x chains, each chain's blocks on one XCD (step_block); 0: 2-D grid
     int seg, nseg;                // block-sum prefix: S blocks per segment, ceil(B / S) segments (<= kMaxSegments)
     size_t hist_stride, anc_stride, wstride, bstride;
     double cert_k;                // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp)

@@ -27,8 +27,9 @@ __global__ __launch_bounds__(WG) void pf_init_kernel(StepArgs a) {
     using Sh = Shape<MODEL, G>;
     constexpr int C = Sh::C;
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int chain = a.chain0 + (int)blockIdx.y;
-    const int j = blockIdx.x * WG + threadIdx.x;
+    const BlockPos bp = step_block(a);
+    const int chain = bp.chain;
+    const int j = bp.b * WG + threadIdx.x;
     if (a.status[chain] != 0) return;
     const ChainParam cp = a.cp[chain];
     double x[C];
@@ -53,7 +54,7 @@ __global__ __launch_bounds__(WG) void pf_init_kernel(StepArgs a) {
         for (int c = 0; c < C; ++c) h[c] = (int32_t)x[c];
         a.ancestry[(size_t)chain * a.anc_stride + j] = 0;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) a.log_zeta[(size_t)chain * a.T] = 0.0;
+    if (bp.b == 0 && threadIdx.x == 0) a.log_zeta[(size_t)chain * a.T] = 0.0;
     if (a.T > 1) {
         double w = 0.0;
         if (j < a.N) w = particle_weight<MODEL, G, OBS>(x, a.Y, cp, a.lf, a.lf_max);
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(WG) void pf_init_kernel(StepArgs a) {
         const double loc = block_inclusive_scan<WG>(w, smem);
         a.wraw[wbase + j] = w;
         a.wloc[wbase + j] = loc;
-        if (threadIdx.x == WG - 1) a.bsum[(size_t)chain * a.bstride + blockIdx.x] = loc;
+        if (threadIdx.x == WG - 1) a.bsum[(size_t)chain * a.bstride + bp.b] = loc;
     }
 }
 
@@ -75,9 +76,10 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
     double* red = smem + 2 * kLogTabEntries;             // WG/64 (+pad)
     double* seg_start = red + 16;                        // S = 1: bsum [B] then bpex [B + WG]; else nseg + nseg
     double* seg_end = seg_start + a.nseg;
-    const int chain = a.chain0 + (int)blockIdx.y;
+    const BlockPos bp = step_block(a);
+    const int chain = bp.chain;
     const int tid = threadIdx.x;
-    const int j = blockIdx.x * WG + tid;
+    const int j = bp.b * WG + tid;
     if (a.status[chain] != 0) return;
     const ChainParam cp = a.cp[chain];
     const int prev = (p - 1) & 1, cur = p & 1;
@@ -91,13 +93,13 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
     const double total = (a.seg == 1) ? scan_block_sums<WG>(a.bsum + bprev, a.B, seg_start + a.B, seg_start, red)
                                       : scan_segments(a.bsum + bprev, a.B, a.seg, a.nseg, seg_start, seg_end);
     if (!(total > 0.0)) {  // all weights 0 or NaN: numpy raises ValueError -> (None, None, None), :187-192
-        if (blockIdx.x == 0 && tid == 0) {
+        if (bp.b == 0 && tid == 0) {
             a.status[chain] = 1;
             a.log_zeta[(size_t)chain * a.T + p] = -__builtin_inf();
         }
         return;
     }
-    if (blockIdx.x == 0 && tid == 0)
+    if (bp.b == 0 && tid == 0)
         a.log_zeta[(size_t)chain * a.T + p] = a.log_zeta[(size_t)chain * a.T + p - 1] + log(total / (double)a.N);
 
     int nev = 0, iters = 0, exact = 0;
@@ -208,7 +210,7 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
         const double loc = block_inclusive_scan<WG>(w, red);
         a.wraw[wcur + j] = w;
         a.wloc[wcur + j] = loc;
-        if (tid == WG - 1) a.bsum[bcur + blockIdx.x] = loc;
+        if (tid == WG - 1) a.bsum[bcur + bp.b] = loc;
     }
 }
 
@@ -366,7 +368,7 @@ static hipError_t launch_filter_t(const StepArgs& a, int n_chains, const FilterS
         ag.chain0 = (int)((long)n_chains * g / S);
         const int n_g = (int)((long)n_chains * (g + 1) / S) - ag.chain0;
         const hipStream_t s = fs.s[g];
-        const dim3 grid(a.B, n_g), block(WG);
+        const dim3 grid = a.xcd_map ? dim3(a.B * n_g) : dim3(a.B, n_g), block(WG);
         if (g == 0 && fs.ev_init) (void)hipEventRecord(fs.ev_init, s);
         hipLaunchKernelGGL((pf_init_kernel<MODEL, G, OBS, WG>), grid, block, lds, s, ag);
         if (g == 0 && fs.ev_step0) (void)hipEventRecord(fs.ev_step0, s);

@@ -2,8 +2,28 @@
 // (epipf_kernels.hip) and the lane-group step kernel (epipf_group.hip).
 #pragma once
 #include "epipf_device.hpp"
+#include "epipf_internal.hpp"
 
 namespace epipf {
+
+// (chain, particle block) of this workgroup.  2-D grid: (blockIdx.y, blockIdx.x).  XCD-aware 1-D grid of B x chains
+// (a.xcd_map): the dispatcher deals workgroups round-robin over the 8 XCDs (MI355X_MICROARCH.md, observed; which XCD
+// gets block 0 is not fixed), so the blocks p = l (mod 8) share one XCD and its L2.  Label l takes a contiguous range
+// of the chain-major block order -- whole chains when B x chains is a multiple of 8 chains' blocks -- so a chain's
+// blocks read its block sums, in-block prefixes and parent states (written by the same blocks' previous step) from
+// one L2 instead of from eight.  A bijection for any grid size (label l holds q + [l < r] blocks), so placement only
+// changes speed.
+struct BlockPos {
+    int chain, b;
+};
+__device__ __forceinline__ BlockPos step_block(const StepArgs& a) {
+    if (!a.xcd_map) return {a.chain0 + (int)blockIdx.y, (int)blockIdx.x};
+    const int total = (int)gridDim.x, p = (int)blockIdx.x;
+    const int q = total >> 3, r = total & 7, l = p & 7;
+    const int L = l * q + min(l, r) + (p >> 3);
+    const int c = L / a.B;
+    return {a.chain0 + c, L - c * a.B};
+}
 
 // LDS ordering between the lanes that run a helper: the whole block (__syncthreads), or only the calling wave
 // (WAVE = true: the lane-group kernel runs these on its first wave while the other waves wait at a block barrier).
