@@ -1,7 +1,8 @@
 // epipf_kernels.hip -- the particle-filter kernels for MI355X (gfx950) and their launchers.
 //
-// One filter step (pmcmc.py:177-231) is ONE kernel launch, batched over independent chains
-// (grid.y = chain, grid.x = particle block of WG lanes, one particle per lane):
+// One filter step (pmcmc.py:177-231) is ONE kernel launch, batched over independent chains: a 1-D grid of
+// (chain, particle block of WG lanes) pairs, one particle per lane, placed so that each chain's blocks share one
+// XCD's L2 (step_block, epipf_step.hpp; EPIPF_XCD_MAP=0: the 2-D grid y = chain, x = block):
 //
 //   step p:  [scan of the previous step's block sums in LDS -> total, log-likelihood]
 //            [multinomial draw U_j -> certified two-level CDF search -> ancestor a_j]   (pmcmc.py:183-193)
