@@ -811,11 +811,15 @@ int epipf_abc(epipf_ctx* c, const double* Y, int T, int no_of_samples, double th
     *trials_out = 0;
     *accepted_out = 0;
     if (no_of_samples == 0) return EPIPF_OK;
-    // batch sizes: fixed, or 64k trials first, then 1.25x the trials the observed acceptance rate predicts for
-    // the samples still missing (x4 while nothing is accepted), within [16k, 1M] and a day table < 4 GiB
+    // batch sizes: fixed, or 256k trials first, then 1.25x the trials the observed acceptance rate predicts for
+    // the samples still missing (x4 while nothing is accepted), within [256k, 1M] and a day table < 4 GiB.  A launch
+    // lasts at least as long as its longest trials (~5 ms at the reference's setting), and below ~4 waves per SIMD
+    // the exact f64 trial loop is latency-bound: 64k trials take 5.2 ms, 256k 7.0 ms (1.27e7 vs 3.74e7 trials/s,
+    // profiles/r2p_abc_batch_sweep.jsonl), so a smaller batch saves nothing and a second launch costs a whole floor.
     const int64_t cap_days = ((int64_t)1 << 32) / (12 * (int64_t)T);
     const int max_batch = (int)std::max<int64_t>(256, std::min<int64_t>(batch > 0 ? batch : (1 << 20), cap_days));
-    int cur = batch > 0 ? std::min(batch, max_batch) : std::min(1 << 16, max_batch);
+    const int min_batch = std::min(1 << 18, max_batch);
+    int cur = batch > 0 ? std::min(batch, max_batch) : min_batch;
     HIP_TRY(hipSetDevice(c->device));
     if (int rc = abc_buffers(c, T, max_batch, no_of_samples, p)) return rc;
     AbcArgs a = p.args;
@@ -849,7 +853,7 @@ int epipf_abc(epipf_ctx* c, const double* Y, int T, int no_of_samples, double th
         if (batch <= 0) {
             const double want = have > 0 ? 1.25 * (double)(no_of_samples - have) * (double)t / (double)have
                                               : 4.0 * cur;
-            cur = (int)std::max<double>(std::min<double>(want + 1024.0, (double)max_batch), std::min(1 << 14, max_batch));
+            cur = (int)std::max<double>(std::min<double>(want + 1024.0, (double)max_batch), (double)min_batch);
         }
     }
     if (have > 0) {
