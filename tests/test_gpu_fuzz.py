@@ -5,6 +5,8 @@ multinomial and systematic resampling, N from 1 to 3000 (ragged blocks), T from 
 (automatic, 1, 2, 4, 8, 16).  Observations are drawn around the ODE-free "probs x initial state" scale so that most
 filters run to the end and some degenerate; the status, every state and every ancestor must equal the oracle's and the
 log-likelihoods agree within 1e-9.  Needs an MI355X: `-m gpu`."""
+import os
+
 import numpy as np
 import pytest
 
@@ -12,7 +14,9 @@ import oracle
 
 pytestmark = pytest.mark.gpu
 
-CASES = 96
+# EPIPF_FUZZ_CASES / EPIPF_FUZZ_FIRST widen the sweep for an extended run (e.g. 1000 cases from seed 96)
+CASES = int(os.environ.get("EPIPF_FUZZ_CASES", 96))
+FIRST = int(os.environ.get("EPIPF_FUZZ_FIRST", 0))
 
 
 def _case(seed):
@@ -68,7 +72,7 @@ def _case(seed):
                 fidx=fidx, lanes=lanes, resample=resample)
 
 
-@pytest.mark.parametrize("seed", range(CASES))
+@pytest.mark.parametrize("seed", range(FIRST, FIRST + CASES))
 def test_random_filters_match_oracle(seed):
     from epipf.engine import Engine, model_id, theta_vector
     a = _case(seed)
