@@ -6,6 +6,10 @@
   warm_start              tests/test_pmcmc_noisy.py:32-40 (and tests/test_under.py:37-49): start at the
                           last draw, proposal covariance from the unique burned-in, thinned draws (ddof=0)
   gelman_rubin            helpers.py:15-43 gelman_rubin_test (potential scale reduction per parameter)
+  hdi / mean_credible_interval, running_mean, posterior_mse
+                          helpers.py:5-13, :46-48, :51-54 -- the reference's posterior summaries (its HDI is
+                          arviz's, which is not installed: restated as arviz computes it, the narrowest interval
+                          holding floor(0.95 n) + 1 sorted draws)
 """
 import os
 
@@ -72,3 +76,33 @@ def gelman_rubin(chains):
     B = N / (M - 1) * ((means - theta_hat) ** 2).sum(axis=0)
     V = (N - 1) / N * W + (M + 1) / (M * N) * B
     return np.sqrt(V / W)
+
+
+def hdi(samples, hdi_prob=0.95):
+    """arviz.hdi of the flattened draws (a 2-D array is (chain, draw), as arviz reads it): with the draws sorted,
+    k = floor(hdi_prob n) and the interval [x_i, x_{i+k}] of least width, the first one on ties."""
+    x = np.sort(np.asarray(samples, dtype=np.float64).reshape(-1))
+    n = x.size
+    k = int(np.floor(hdi_prob * n))
+    width = x[k:] - x[:n - k]
+    i = int(np.argmin(width))
+    return np.array([x[i], x[i + k]])
+
+
+def mean_credible_interval(data, alpha=0.95):
+    """helpers.py:5-13: (mean, hdi_low, hdi_high); the mean per row for 2-D data, the HDI (95%, as the reference:
+    it never passes `alpha` on) over all draws."""
+    a = np.array(data)
+    m = np.mean(a, axis=1) if len(a.shape) == 2 else np.mean(a)
+    return (m, *hdi(a, 0.95))
+
+
+def running_mean(x, N):
+    """helpers.py:46-48: the length-N moving average of x."""
+    cumsum = np.cumsum(np.insert(x, 0, 0))
+    return (cumsum[N:] - cumsum[:-N]) / float(N)
+
+
+def posterior_mse(true_prm, chain):
+    """helpers.py:51-54: mean squared error of the draws against the true parameter."""
+    return np.mean((chain - true_prm) ** 2)
