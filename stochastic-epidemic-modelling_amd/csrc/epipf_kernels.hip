@@ -369,7 +369,9 @@ static hipError_t launch_filter_t(const StepArgs& a, int n_chains, const FilterS
         ag.chain0 = (int)((long)n_chains * g / S);
         const int n_g = (int)((long)n_chains * (g + 1) / S) - ag.chain0;
         const hipStream_t s = fs.s[g];
-        const dim3 grid = a.xcd_map ? dim3(a.B * n_g) : dim3(a.B, n_g), block(WG);
+        // the 1-D XCD-aware grid while its work-items fit HIP's 32-bit x extent (with room for lane-group blocks)
+        ag.xcd_map = a.xcd_map && (long)a.B * n_g * WG * std::max(1, a.lanes) < (1L << 31);
+        const dim3 grid = ag.xcd_map ? dim3(a.B * n_g) : dim3(a.B, n_g), block(WG);
         if (g == 0 && fs.ev_init) (void)hipEventRecord(fs.ev_init, s);
         hipLaunchKernelGGL((pf_init_kernel<MODEL, G, OBS, WG>), grid, block, lds, s, ag);
         if (g == 0 && fs.ev_step0) (void)hipEventRecord(fs.ev_step0, s);
