@@ -935,7 +935,40 @@ __device__ __forceinline__ double cert_halfwidth(int i, double v, double cert_k)
 // only the final bracket is evaluated on v = prefix / total.  Where the two orders disagree (a prefix within an
 // ulp of U * total) the candidate is off by one, its bracket test fails and the exact fallback decides, so the
 // result is still numpy's.
-template <int WG>
+// In-block level: the first m in [0, WG - 1) with base + L[m] > Ut, else WG - 1 (L: the block's in-block inclusive
+// prefix, non-decreasing, so base + L[m] is too).  Binary search: log2(WG) dependent loads.  FLAT (WG = 64, the
+// latency-bound lane-group kernel): the same index from two rounds of 7 independent loads -- the sub-block maxima
+// L[8i + 7], i < 7, give the sub-block s (the count of those <= Ut), then L[8s + j], j < 7, the offset (the count of
+// those <= Ut); counting a monotone predicate is the binary search's answer.
+template <int WG, bool FLAT = false>
+__device__ __forceinline__ int inblock_search(double base, const double* __restrict__ L, double Ut) {
+    if constexpr (FLAT) {
+        static_assert(WG == 64, "8 x 8 sub-blocks");
+        double c[7];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) c[i] = L[8 * i + 7];
+        int s = 0;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) s += (base + c[i] > Ut) ? 0 : 1;
+        const double* Ls = L + 8 * s;
+        double f[7];
+#pragma unroll
+        for (int j = 0; j < 7; ++j) f[j] = Ls[j];
+        int o = 0;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) o += (base + f[j] > Ut) ? 0 : 1;
+        return 8 * s + o;
+    } else {
+        int l = 0, h = WG - 1;
+        while (l < h) {
+            const int m = (l + h) >> 1;
+            if (base + L[m] > Ut) h = m; else l = m + 1;
+        }
+        return l;
+    }
+}
+
+template <int WG, bool FLAT = false>
 __device__ __forceinline__ int resample_search(double U, const double* bpex, const double* bsum, int B,
                                                double total, const double* wloc, int N, double cert_k,
                                                bool& certified) {
@@ -948,11 +981,7 @@ __device__ __forceinline__ int resample_search(double U, const double* bpex, con
     const int b = lo;
     const double base = bpex[b];
     const double* L = wloc + (size_t)b * WG;
-    int l = 0, h = WG - 1;
-    while (l < h) {
-        const int m = (l + h) >> 1;
-        if (base + L[m] > Ut) h = m; else l = m + 1;
-    }
+    const int l = inblock_search<WG, FLAT>(base, L, Ut);
     const int a = b * WG + l;
     const double va = (base + L[l]) / total;
     const double vp = (l > 0) ? (base + L[l - 1]) / total
@@ -966,6 +995,7 @@ __device__ __forceinline__ int resample_search(double U, const double* bpex, con
 // segment ends seg_end[k] (S blocks per segment), level 2 walks the <= S block sums of the segment from global
 // memory with the scan's own additions (so every value equals the scan's), level 3 the block's in-block prefix.
 // With S = 1 this is resample_search above, value for value (seg_start = bpex, seg_end = bpex + bsum).
+template <bool FLAT = false>
 __device__ __forceinline__ int resample_search_seg(double U, const double* seg_start, const double* seg_end, int nseg,
                                                    int S, const double* __restrict__ bsum_g, int B, double total,
                                                    const double* __restrict__ wloc, int WGB, int N, double cert_k,
@@ -989,10 +1019,16 @@ __device__ __forceinline__ int resample_search_seg(double U, const double* seg_s
         }
     }
     const double* L = wloc + (size_t)b * WGB;
-    int l = 0, h = WGB - 1;
-    while (l < h) {
-        const int m = (l + h) >> 1;
-        if (base + L[m] > Ut) h = m; else l = m + 1;
+    int l;
+    if (FLAT && WGB == 64) {
+        l = inblock_search<64, true>(base, L, Ut);
+    } else {
+        l = 0;
+        int h = WGB - 1;
+        while (l < h) {
+            const int m = (l + h) >> 1;
+            if (base + L[m] > Ut) h = m; else l = m + 1;
+        }
     }
     const int a = b * WGB + l;
     const double va = (base + L[l]) / total;

@@ -302,10 +302,10 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
                     U = ((double)j + u01(r.x, r.y)) / (double)a.N;
                 }
                 if (a.seg == 1)
-                    anc = resample_search<64>(U, seg_start + a.B, seg_start, a.B, total, a.wloc + wprev, a.N, a.cert_k,
+                    anc = resample_search<64, true>(U, seg_start + a.B, seg_start, a.B, total, a.wloc + wprev, a.N, a.cert_k,
                                               certified);
                 else
-                    anc = resample_search_seg(U, seg_start, seg_end, a.nseg, a.seg, a.bsum + bprev, a.B, total,
+                    anc = resample_search_seg<true>(U, seg_start, seg_end, a.nseg, a.seg, a.bsum + bprev, a.B, total,
                                               a.wloc + wprev, 64, a.N, a.cert_k, certified);
             }
             if (__any(!certified)) {
