@@ -1,5 +1,5 @@
 #!/bin/bash
-# Flat in-block resampling search in the lane-group kernel: lane/parity tests, then A/B vs lib_old (one and few
+# Lane-group kernel change: lane/parity tests, then A/B vs lib_old (one and few
 # chains, configs 2 and 5).
 set -u
 cd "${GRAFT_REPO_ROOT}"
