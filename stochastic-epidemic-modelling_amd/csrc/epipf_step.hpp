@@ -10,9 +10,9 @@ namespace epipf {
 // (a.xcd_map): the dispatcher deals workgroups round-robin over the 8 XCDs (MI355X_MICROARCH.md, observed; which XCD
 // gets block 0 is not fixed), so the blocks p = l (mod 8) share one XCD and its L2.  Label l takes a contiguous range
 // of the chain-major block order -- whole chains when B x chains is a multiple of 8 chains' blocks -- so a chain's
-// blocks read its block sums, in-block prefixes and parent states (written by the same blocks' previous step) from
-// one L2 instead of from eight.  A bijection for any grid size (label l holds q + [l < r] blocks), so placement only
-// changes speed.
+// blocks fetch its block sums, in-block prefixes and parent states (the previous step's) into one L2 instead of
+// eight, and find them already there when consecutive launches deal the label to the same XCD.  A bijection for any
+// grid size (label l holds q + [l < r] blocks), so placement only changes speed.
 struct BlockPos {
     int chain, b;
 };
