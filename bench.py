@@ -43,9 +43,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--single-chain", action=argparse.BooleanOptionalAction, default=True,
                     help="also time 1 chain/GPU (N=1 only): one filter per MH iteration, and speculative MH (extra fields)")
-    ap.add_argument("--pipelines", type=int, default=int(os.environ.get("EPIPF_BENCH_PIPELINES", 1)),
+    ap.add_argument("--pipelines", type=int, default=int(os.environ.get("EPIPF_BENCH_PIPELINES", 0)),
                     help="chain groups on their own engine + host thread, so each group's MH host work overlaps the "
-                         "others' filters (epipf.pmcmc.run_pipelined); 1 = one lockstep sampler")
+                         "others' filters (epipf.pmcmc.run_pipelined); 1 = one lockstep sampler; 0 = automatic: 2 "
+                         "where the MH step is host-bound (config 1: tiny filters), else 1 (DESIGN.md §6)")
     ap.add_argument("--prefetch", type=int, default=16, help="filter slots per round of the speculative single chain")
     ap.add_argument("--prefetch-iters", type=int, default=60, help="MH iterations timed for the speculative chain")
     return ap.parse_args()
@@ -153,7 +154,8 @@ def main():
     N, T = (args.particles or meta["N"]), Y.shape[0]
     C = args.chains
     gid = shard(C * world, world, rank)                              # global chain ids of this rank
-    P = max(1, min(args.pipelines, C))
+    pipelines = args.pipelines or (2 if N * T <= 20000 else 1)   # host-bound MH steps: overlap two samplers' host work
+    P = max(1, min(pipelines, C))
     streams_env = max(1, min(int(os.environ.get("EPIPF_STREAMS", 4)), 8))
     samplers = []
     for k in range(P):                                               # contiguous chain groups, one engine each
