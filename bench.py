@@ -126,23 +126,68 @@ def cpu_baseline(Y, meta, N, seconds):
     return base
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_command(argv, gpus, port):
+    """The command `bench.py --gpus N` (N > 1, no WORLD_SIZE in the environment) runs as its child: one rank per GPU
+    under torch.distributed.run on this node, the same form the driver uses, with this invocation's arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(args, argv):
+    """Parent side of a self-launched N-GPU bench.  Runs before anything initialises the GPU (counting devices does
+    not on this image), starts the ranks as a child process (never an exec) and returns its exit code; the ranks'
+    output (rank 0's JSON line) passes straight through."""
+    import subprocess
+    backend = os.environ.get("EPIPF_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        import torch
+        ndev = torch.cuda.device_count()
+        if args.gpus > ndev:
+            print(f"bench.py: --gpus {args.gpus} but this node has {ndev} GPU(s); the nccl (RCCL) backend needs one "
+                  f"GPU per rank", file=sys.stderr, flush=True)
+            return 2
+    cmd = launcher_command(argv, args.gpus, free_port())
+    print(f"bench.py: launching {args.gpus} ranks ({backend}): {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=dict(os.environ, EPIPF_BENCH_LAUNCHED="1"))
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("EPIPF_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI; gloo only for rehearsals
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    if "WORLD_SIZE" in os.environ and world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     dist = None
     # EPIPF_BENCH_DIST=1: the distributed path (process group, max/sum reductions, RCCL all-gather) even at one rank,
     # so that a one-GPU box rehearses the RCCL code of the driver's N-GPU runs (scripts/rccl_bench_check.sh)
     force_dist = os.environ.get("EPIPF_BENCH_DIST") == "1"
+    devices = [[platform.node(), local]]
     if world > 1 or force_dist:
         import torch
         import torch.distributed as dist
         ndev = torch.cuda.device_count()
-        local = local % max(ndev, 1)      # one GPU per rank on a full node; ranks share GPUs in rehearsals
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        if backend == "nccl" and local_world > ndev:
+            sys.exit(f"bench.py: {local_world} ranks on this node but {ndev} GPU(s); nccl (RCCL) needs one GPU per rank")
+        local = local % max(ndev, 1)      # one GPU per rank on a full node; ranks share GPUs in gloo rehearsals
         torch.cuda.set_device(local)
         dist.init_process_group(backend)
+        assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
+        devices = [None] * world
+        dist.all_gather_object(devices, [platform.node(), local])
+        if backend == "nccl":                                       # one distinct GPU per rank
+            assert len({tuple(d) for d in devices}) == world, f"ranks share a GPU under nccl: {devices}"
     import torch
 
     from epipf import datasets
@@ -224,12 +269,6 @@ def main():
     else:
         filters_all = filters
     value = filters_all * N * T / dt
-    # Gelman-Rubin R-hat of every chain's gathered draws (helpers.py:15-43), outside the timed region
-    from epipf.chains_io import gelman_rubin
-    from epipf.distributed import unpack_draws
-    d_par = samplers[0].d
-    g_th, _ = unpack_draws(gathered, d_par)
-    rhat = gelman_rubin(list(g_th)) if g_th.shape[0] >= 2 and g_th.shape[1] >= 2 else None
 
     # roofline of the dominant kernel: pf_step_kernel (resample + gather + SSA + weight + in-block scan)
     # One filter step of every chain on this rank is issued as `streams` concurrent pf_step_kernel launches, one
@@ -257,8 +296,11 @@ def main():
             pmc = {}
     # SSA lanes per particle of the timed runs (1: pf_step_kernel; > 1: the lane-group kernel)
     lanes = int(engines[0].stats()["last_lanes"]) or 1
-    # the committed PMC pass profiles the default bench (config 2, 256 chains per GPU, one lane per particle)
-    if pmc.get("config", 2) == args.config and pmc.get("chains_per_gpu", 256) == C and lanes == 1:
+    # the committed PMC pass profiles the default bench (config 2, 256 chains per GPU, one lane per particle) on one
+    # build of the library: it is used only when the library timed here carries the same build id (a hash of every
+    # kernel source and flag, epipf_build_id); after any kernel change it reads as stale and the PMC fields are null
+    pmc_current = pmc.get("build_id") == _lib.build_id()
+    if pmc_current and pmc.get("config", 2) == args.config and pmc.get("chains_per_gpu", 256) == C and lanes == 1:
         # MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE counts half the bytes of a coalesced read stream, so
         # `traffic` doubles the read side (FETCH x 2 + WRITE); the raw counter sum is `traffic_raw`
         per_unit = pmc.get("hbm_bytes_per_particle_step_read_doubled")
@@ -334,8 +376,8 @@ def main():
         base = cpu_baseline(Y, meta, N, args.cpu_baseline_seconds)
 
     if rank == 0:
-        # distinct GPUs, not ranks: rehearsals may run several ranks on one device
-        n_gpus = min(world, torch.cuda.device_count()) if world > 1 else 1
+        # distinct GPUs, not ranks: (host, device) pairs over all ranks (gloo rehearsals put several ranks on one)
+        n_gpus = len({tuple(d) for d in devices})
         line = {
             "metric": f"particle-steps/sec (N_particles x T_obs x MH-iters) on {MODEL_NAMES[meta['model']]} PMCMC",
             "value": value,
@@ -372,12 +414,20 @@ def main():
             "ssa_lane_utilisation": lane_use if lanes == 1 else None,
             "lanes_per_particle": lanes,
             "resample_fallbacks": st["resample_fallbacks"],
+            # draws of the timed region whose uniform lies within scipy's error envelope of a CDF boundary: the only
+            # draws where the reference's own weights could pick another ancestor; of all draws
+            "resample_ref_ambiguous": st["resample_ref_ambiguous"],
+            "resample_draws": filters * N * (T - 1),
+            "library_build_id": _lib.build_id(),
+            "pmc_profile": {"build_id": pmc.get("build_id"), "current": pmc_current},
             "events_per_particle_step": cst["events"] / cst["particle_steps"] if cst["particle_steps"] else None,
             # particle-steps the certified f32 SSA path handed to the exact loop, and waves that waited on one
             "ssa_exact_particle_frac": cst["ssa_exact_lanes"] / cst["particle_steps"] if cst["particle_steps"] else None,
             "ssa_exact_wave_frac": cst["ssa_exact_waves"] * 64 / cst["particle_steps"] if cst["particle_steps"] else None,
+            # every rank's posterior draws after the RCCL all-gather (R-hat is not reported: a bench run is tens of
+            # iterations from a fixed start, far too short for a convergence diagnostic)
             "gathered_draws_shape": list(gathered.shape),
-            "gathered_rhat": None if rhat is None else [float(x) for x in rhat],
+            "rank_devices": [f"{h}:{d}" for h, d in devices],
             "cpu_baseline": base,
         }
         if single is not None:

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define EPIPF_ABI_VERSION 5
+#define EPIPF_ABI_VERSION 6
 
 /* return codes */
 #define EPIPF_OK 0
@@ -92,6 +92,10 @@ typedef struct {
     int64_t last_lanes;          /* SSA lanes per particle of the last epipf_run (1: one-lane step kernel; 2..16: the
                                     lane-group step kernel, epipf_set_lanes) */
     int64_t last_lane_events;    /* events per lane per chunk of that run's lane-group kernel (1 for the one-lane one) */
+    int64_t resample_ref_ambiguous; /* resampling draws whose uniform lies so close to a CDF boundary that scipy's own
+                                       weights (within the measured envelope of their error) could pick
+                                       a neighbouring ancestor: a diagnostic count, always on; the draw itself is the
+                                       numpy answer over the device's weights */
 } epipf_stats;
 
 /* groups: G for the subgroup models (1 <= G <= 4), ignored (1) for SIR/SEIR.
@@ -194,6 +198,9 @@ int epipf_reset_stats(epipf_ctx* ctx);
 
 const char* epipf_last_error(void);
 int epipf_abi_version(void);
+/* Hash of the library's sources and build flags (16 hex digits; "...-debug" for libepipf_debug.so).  Profiles taken
+ * on one build are trusted by bench.py only for the same id. */
+const char* epipf_build_id(void);
 int epipf_device_count(void);
 
 #ifdef __cplusplus

@@ -17,13 +17,15 @@
  * Third-party arithmetic restated here (absent as C in /root/reference):
  *   numpy 2.2 legacy RandomState.exponential(scale) = scale * (-log(1.0 - U))   (glibc log)
  *   numpy 2.2 legacy RandomState.choice(a, size, p)  = searchsorted(cumsum(p)/cumsum(p)[-1], U, 'right')
- *   scipy 1.15 binom.pmf(k, n, p)  -> exp(lgamma(n+1) - lgamma(k+1) - lgamma(n-k+1) + k log p + (n-k) log1p(-p))
- *                                     (Boost in scipy; agrees to ~1e-11 relative)
+ *   scipy 1.15 binom.pmf(k, n, p)  -> exp(log n! - log k! - log (n-k)! + k log p + (n-k) log1p(-p)), the log
+ *                                     carried as hi + lo from binary128 tables (Boost in scipy; within scipy's own
+ *                                     error, <= ~1e-12 relative at n <= 5e4, of it: DESIGN.md §4)
  *   scipy 1.15 norm.pdf(y, loc, scale) = exp(-z*z/2) / 2.5066282746310002 / scale,  z = (y-loc)/scale
  *
  * Compile with -ffp-contract=off: every multiply/add/divide must round exactly like CPython/numpy.
  */
 #include <math.h>
+#include <quadmath.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -226,17 +228,75 @@ int oracle_simulate_path(int model, int G, int n, const int32_t* states_in, cons
     return 0;
 }
 
-/* ------------------------------------------------------------------ observation weights, pmcmc.py:178-181 */
-static double binom_pmf(double k, double n, double p, double logp, double log1mp) {
-    if (!(p >= 0.0 && p <= 1.0)) return NAN;                   /* scipy _argcheck -> nan */
-    if (k < 0.0 || k > n || k != floor(k)) return 0.0;         /* outside support / non-integral k */
-    if (p == 0.0) return (k == 0.0) ? 1.0 : 0.0;
-    if (p == 1.0) return (k == n) ? 1.0 : 0.0;
-    double a = lgamma(n + 1.0) - lgamma(k + 1.0);
-    a = a - lgamma((n - k) + 1.0);
-    double b = k * logp;
-    double c = (n - k) * log1mp;
-    return exp(a + (b + c));
+/* ------------------------------------------------------------------ observation weights, pmcmc.py:178-181
+ * binom.pmf as exp of its log closed form, log n! - log k! - log (n-k)! + k log p + (n-k) log1p(-p), carried as
+ * an unevaluated hi + lo pair: log-factorials and log p / log1p(-p) are binary128 values (libquadmath) split
+ * into two doubles, the roundings of the hi-part sums and products are recovered exactly (two-sum, fma) and the
+ * lo terms summed in double.  The pmf is then exp(hi) (1 + lo): the true pmf to within exp's rounding, closer
+ * than scipy's own Boost evaluation (<= ~1e-12 relative at n <= 5e4, scripts/scipy_pmf_envelope.py). */
+typedef struct { double hi, lo; } logw_t;          /* hi = -inf: pmf 0; NaN: bad p */
+typedef struct { double logp, logp_lo, log1mp, log1mp_lo; } logp_t;
+
+static void split128(__float128 q, double* hi, double* lo) {
+    const double h = (double)q;
+    *hi = h;
+    *lo = isfinite(h) ? (double)(q - (__float128)h) : 0.0;
+}
+static logp_t log_p_split(double p) {
+    logp_t r;
+    split128(logq((__float128)p), &r.logp, &r.logp_lo);
+    split128(log1pq(-(__float128)p), &r.log1mp, &r.log1mp_lo);
+    return r;
+}
+/* (hi, lo) of log n! for n = 0..n_max, interleaved */
+static double* logfact_table(int n_max) {
+    double* t = (double*)malloc(sizeof(double) * 2 * ((size_t)n_max + 1));
+    for (int n = 0; n <= n_max; ++n) split128(lgammaq((__float128)n + 1), &t[2 * (size_t)n], &t[2 * (size_t)n + 1]);
+    return t;
+}
+static void two_sum(double a, double b, double* s, double* e) {
+    *s = a + b;
+    const double bb = *s - a;
+    *e = (a - (*s - bb)) + (b - bb);
+}
+/* the regular case from the table entries (hi, lo) of log n!, log k!, log (n-k)! */
+static logw_t binom_logpmf_entries(double k, double n, const logp_t* lp, const double* fn, const double* fk,
+                                   const double* fm) {
+    const double m = n - k;
+    double s1, e1, s2, e2, s3, e3, s4, e4;
+    two_sum(fn[0], -fk[0], &s1, &e1);
+    two_sum(s1, -fm[0], &s2, &e2);
+    const double p1 = k * lp->logp, f1 = fma(k, lp->logp, -p1);   /* exact products: p1 + f1 = k * logp */
+    const double p2 = m * lp->log1mp, f2 = fma(m, lp->log1mp, -p2);
+    two_sum(p1, p2, &s3, &e3);
+    two_sum(s2, s3, &s4, &e4);
+    double lo = (fn[1] - fk[1]) - fm[1];
+    lo = lo + ((e1 + e2) + (e3 + e4));
+    lo = lo + (f1 + f2);
+    lo = lo + (k * lp->logp_lo + m * lp->log1mp_lo);
+    logw_t r = {s4, lo};
+    return r;
+}
+static logw_t binom_logpmf(double k, double n, double p, const logp_t* lp, const double* lf, int lf_max) {
+    logw_t r = {0.0, 0.0};
+    if (!(p >= 0.0 && p <= 1.0)) { r.hi = NAN; return r; }                  /* scipy _argcheck -> nan */
+    if (k < 0.0 || k > n || k != floor(k)) { r.hi = -INFINITY; return r; } /* outside support / non-integral k */
+    if (p == 0.0) { r.hi = (k == 0.0) ? 0.0 : -INFINITY; return r; }
+    if (p == 1.0) { r.hi = (k == n) ? 0.0 : -INFINITY; return r; }
+    if (!lf) return r;                                     /* regular case, no table: the caller supplies entries */
+    int ni = (int)n, ki = (int)k, mi = ni - ki;
+    ni = ni < 0 ? 0 : ni > lf_max ? lf_max : ni;
+    ki = ki < 0 ? 0 : ki > lf_max ? lf_max : ki;
+    mi = mi < 0 ? 0 : mi > lf_max ? lf_max : mi;
+    return binom_logpmf_entries(k, n, lp, &lf[2 * ni], &lf[2 * ki], &lf[2 * mi]);
+}
+static int logw_less(logw_t a, logw_t b) {
+    if (a.hi != b.hi) {
+        const double d = a.hi - b.hi;
+        if (!(fabs(d) < 1.0)) return a.hi < b.hi;
+        return d + (a.lo - b.lo) < 0.0;
+    }
+    return a.lo < b.lo;
 }
 static double norm_pdf(double y, double x, double probs) {
     double scale = probs * x + 0.0001;                         /* pmcmc.py:181 */
@@ -244,17 +304,28 @@ static double norm_pdf(double y, double x, double probs) {
     double z = (y - x) / scale;
     return (exp(-(z * z) / 2.0) / 2.5066282746310002) / scale;
 }
-/* min over observed columns of the per-column likelihood (np.min propagates NaN) */
-static double weight(int obs, const double* yrow, const double* xobs, int K, double probs, double logp,
-                     double log1mp) {
-    double w = 0.0;
-    for (int i = 0; i < K; ++i) {
-        double wi = (obs == OBS_BINOMIAL) ? binom_pmf(yrow[i], xobs[i], probs, logp, log1mp)
-                                          : norm_pdf(yrow[i], xobs[i], probs);
-        if (i == 0 || isnan(wi)) w = wi;
-        else if (!isnan(w) && wi < w) w = wi;
+/* min over observed columns of the per-column likelihood (np.min propagates NaN); binomial: min of the logs,
+ * exponentiated once (exp is monotone) */
+static double weight(int obs, const double* yrow, const double* xobs, int K, double probs, const logp_t* lp,
+                     const double* lf, int lf_max) {
+    if (obs != OBS_BINOMIAL) {
+        double w = 0.0;
+        for (int i = 0; i < K; ++i) {
+            double wi = norm_pdf(yrow[i], xobs[i], probs);
+            if (i == 0 || isnan(wi)) w = wi;
+            else if (!isnan(w) && wi < w) w = wi;
+        }
+        return w;
     }
-    return w;
+    logw_t L = {0.0, 0.0};
+    for (int i = 0; i < K; ++i) {
+        logw_t li = binom_logpmf(yrow[i], xobs[i], probs, lp, lf, lf_max);
+        if (i == 0 || isnan(li.hi)) L = li;
+        else if (!isnan(L.hi) && logw_less(li, L)) L = li;
+    }
+    if (isnan(L.hi)) return L.hi;
+    const double e = exp(L.hi);
+    return fma(e, L.lo, e);
 }
 
 /* numpy legacy choice(range(N), N, p=w/sum(w)) given the uniforms, pmcmc.py:185-190.
@@ -293,7 +364,11 @@ int oracle_particle_filter(int model, int G, int N, int T, int K, const double* 
     double* w = (double*)malloc(sizeof(double) * (size_t)N);
     double* u = (double*)malloc(sizeof(double) * (size_t)N);
     int32_t* anc = (int32_t*)malloc(sizeof(int32_t) * (size_t)N);
-    const double logp = log(probs), log1mp = log1p(-probs);
+    const logp_t lp = log_p_split(probs);
+    double pop = 0.0;
+    for (int g = 0; g < Gm; ++g) pop = pop + npop[g];
+    const int lf_max = obs == OBS_BINOMIAL ? (int)pop : 0;      /* counts never exceed the population */
+    double* lf = logfact_table(lf_max);
     long total_events = 0;
     int status = 0;
     uint32_t r[4];
@@ -328,7 +403,7 @@ int oracle_particle_filter(int model, int G, int N, int T, int K, const double* 
             } else {
                 for (int c = 0; c < C; ++c) xo[c] = prev[(size_t)j * C + c];
             }
-            w[j] = weight(obs, Y + (size_t)(p - 1) * K, xo, K, probs, logp, log1mp);
+            w[j] = weight(obs, Y + (size_t)(p - 1) * K, xo, K, probs, &lp, lf, lf_max);
         }
         /* (b) zetas[p] = zetas[p-1] * mean(w), :183 */
         double sw = 0.0;
@@ -362,7 +437,7 @@ int oracle_particle_filter(int model, int G, int N, int T, int K, const double* 
         total_events += ev;
     }
     if (events_out) *events_out = total_events;
-    free(w); free(u); free(anc);
+    free(w); free(u); free(anc); free(lf);
     return status;
 }
 
@@ -389,5 +464,18 @@ void oracle_log_batch(long n, const double* x, double* out) {
 }
 
 /* scalar weight functions, exported so tests can pin them against scipy (tests/golden/kernels_golden.npz) */
-double oracle_binom_pmf(double k, double n, double p) { return binom_pmf(k, n, p, log(p), log1p(-p)); }
+double oracle_binom_pmf(double k, double n, double p) {
+    const logp_t lp = log_p_split(p);
+    logw_t L = binom_logpmf(k, n, p, &lp, NULL, 0);       /* the special cases read no table */
+    if (L.hi == 0.0 && L.lo == 0.0 && p > 0.0 && p < 1.0 && k >= 0.0 && k <= n && k == floor(k)) {
+        double fn[2], fk[2], fm[2];                        /* the three table entries binom_logpmf reads */
+        split128(lgammaq((__float128)(int)n + 1), &fn[0], &fn[1]);
+        split128(lgammaq((__float128)(int)k + 1), &fk[0], &fk[1]);
+        split128(lgammaq((__float128)((int)n - (int)k) + 1), &fm[0], &fm[1]);
+        L = binom_logpmf_entries(k, n, &lp, fn, fk, fm);
+    }
+    if (isnan(L.hi)) return L.hi;
+    const double e = exp(L.hi);
+    return fma(e, L.lo, e);
+}
 double oracle_norm_pdf(double y, double x, double probs) { return norm_pdf(y, x, probs); }

@@ -70,10 +70,19 @@ def main(d):
     lanes = float(meta.get("Grid_Size") or 0)
     if lanes > 0:   # one lane per particle (padding of the last block included: < 0.5% at N = 10^4)
         out["particle_steps_per_launch"] = lanes
+    # the library build these counters belong to (bench.py uses them only for the same build id)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "stochastic-epidemic-modelling_amd"))
+    from epipf import _lib
+    out["build_id"] = _lib.build_id()
+    out.update({k: v for k, v in (("config", CONFIG), ("chains_per_gpu", CHAINS)) if v is not None})
     print(json.dumps(out, indent=1))
     with open(os.path.join(d, "pmc_step_kernel.json"), "w") as f:
         json.dump(out, f, indent=1)
 
+
+CONFIG = int(os.environ["PMC_CONFIG"]) if os.environ.get("PMC_CONFIG") else None        # bench --config profiled
+CHAINS = int(os.environ["PMC_CHAINS"]) if os.environ.get("PMC_CHAINS") else None        # bench --chains profiled
 
 if __name__ == "__main__":
     main(sys.argv[1])

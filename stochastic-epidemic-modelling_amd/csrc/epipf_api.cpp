@@ -127,6 +127,16 @@ static double cert_k(int N, int B, int wg) {
     return (double)N + 2.0 * D + 8.0;
 }
 
+// E: the relative error by which the reference's weights (scipy binom.pmf / norm.pdf) may differ from the device's.
+// Binomial: scipy's Boost evaluation measured against 200-bit truth (scripts/scipy_pmf_envelope.py,
+// profiles/r3_scipy_pmf_envelope.json: at most ~0.6 of this envelope over n <= 2e5, all p) plus the device's own
+// <= 2 ulps; normal: numpy's exp vs the device's plus the divisions, 2^-48 (16 ulps).  An envelope, measured, not
+// proven: the count it drives (resample_ref_ambiguous) is a diagnostic, never a decision.
+static double ref_pmf_envelope(int obs_model, int n_max) {
+    if (obs_model == EPIPF_OBS_NORMAL) return 0x1.0p-48;
+    return 4e-12 + 1e-16 * (double)std::max(n_max, 0);
+}
+
 static int theta_dim(int model, int G) { return model == EPIPF_SIR ? 2 : model == EPIPF_SEIR ? 3 : G * G + 1; }
 
 static void free_ctx(epipf_ctx* c) {
@@ -171,6 +181,13 @@ extern "C" {
 
 const char* epipf_last_error(void) { return g_err.c_str(); }
 int epipf_abi_version(void) { return EPIPF_ABI_VERSION; }
+const char* epipf_build_id(void) {
+#ifdef EPIPF_BUILD_ID
+    return EPIPF_BUILD_ID;
+#else
+    return "unknown";
+#endif
+}
 int epipf_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -296,12 +313,12 @@ int epipf_set_population(epipf_ctx* c, const double* n_population, const double*
     HIP_TRY(hipSetDevice(c->device));
     if (need + 1 > c->lf_cap) {
         if (c->lf) { HIP_TRY(hipStreamSynchronize(c->stream)); (void)hipFree(c->lf); c->lf = nullptr; }
-        if (dalloc(&c->lf, (size_t)need + 1)) return EPIPF_ENOMEM;
+        if (dalloc(&c->lf, 2 * ((size_t)need + 1))) return EPIPF_ENOMEM;
         c->lf_cap = need + 1;
     }
     if (need != c->lf_max) {
-        std::vector<double> lf((size_t)need + 1);
-        for (int n = 0; n <= need; ++n) lf[n] = std::lgamma((double)n + 1.0);   // scipy binom.pmf restatement
+        std::vector<double> lf(2 * ((size_t)need + 1));
+        logfact_table(need, lf.data());                                  // log n! as hi + lo (binom_logpmf)
         HIP_TRY(hipMemcpyAsync(c->lf, lf.data(), sizeof(double) * lf.size(), hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         c->lf_max = need;
@@ -334,8 +351,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
             q.thetaf[i] = (float)v;
         }
         q.probs = probs[ch];
-        q.logp = std::log(probs[ch]);
-        q.log1mp = std::log1p(-probs[ch]);
+        log_p_split(probs[ch], &q.logp, &q.logp_lo, &q.log1mp, &q.log1mp_lo);
         q.k0 = (uint32_t)keys[ch];
         q.k1 = (uint32_t)(keys[ch] >> 32);
         q.f = filter_index[ch];
@@ -353,7 +369,8 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     a.resample_mode = resample_mode; a.count_events = c->profiling >= EPIPF_PROFILE_COUNTERS ? 1 : 0; a.lf_max = c->lf_max;
     a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride; a.wstride = c->wstride; a.bstride = c->bstride;
     a.cert_k = cert_k(c->N, c->B, c->wg);
-    a.Y = c->Y; a.lf = c->lf; a.logtab = c->logtab; a.cp = c->cp; a.hidden = c->hidden; a.ancestry = c->ancestry;
+    a.ref_k = 2.0 * ref_pmf_envelope(obs_model, c->lf_max) * (1.0 + 0x1.0p-10);
+    a.Y = c->Y; a.lf = reinterpret_cast<const double2*>(c->lf); a.logtab = c->logtab; a.cp = c->cp; a.hidden = c->hidden; a.ancestry = c->ancestry;
     a.wraw = c->wraw; a.wloc = c->wloc; a.bsum = c->bsum; a.log_zeta = c->log_zeta; a.status = c->status;
     a.seg = prefix_segment(c->B); a.nseg = (c->B + a.seg - 1) / a.seg;
     a.counters = c->counters;
@@ -366,6 +383,8 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     c->stats.last_lane_events = a.lane_events;
     for (int g = 0; g < kMaxG; ++g) { a.npop[g] = c->npop[g]; a.mu[g] = c->mu[g]; a.emu[g] = c->emu[g]; a.kmax[g] = c->kmax[g]; }
 
+    EPIPF_RANGE_PUSH("epipf_run");
+    struct RangeEnd { ~RangeEnd() { EPIPF_RANGE_POP(); } } range_end;
     FilterStreams fs{};
     fs.n = std::min(c->n_streams, n_chains);
     // Created on first use, not with the context: HIP maps streams onto its few hardware queues in creation order,
@@ -424,7 +443,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
             c->stats.step_kernel_launches += c->T - 1;
         }
     }
-    unsigned long long tot[kNumCounters] = {0, 0, 0, 0, 0, 0};
+    unsigned long long tot[kNumCounters] = {};
     for (int sl = 0; sl < kCounterSlots; ++sl)
         for (int k = 0; k < kNumCounters; ++k) tot[k] += c->h_counters[(size_t)sl * kCounterStride + k];
     c->stats.events = (int64_t)tot[0];
@@ -433,6 +452,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     c->stats.wave_lane_slots = (int64_t)tot[3];
     c->stats.ssa_exact_lanes = (int64_t)tot[4];
     c->stats.ssa_exact_waves = (int64_t)tot[5];
+    c->stats.resample_ref_ambiguous = (int64_t)tot[6];
     c->stats.particle_steps += (int64_t)n_active * c->N * c->T;
     c->stats.filters += n_active;
     c->last_chains = n_chains;
@@ -741,7 +761,7 @@ int abc_read_counters(epipf_ctx* c) {
     HIP_TRY(hipMemcpyAsync(c->h_counters, c->counters, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride,
                            hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    unsigned long long tot[kNumCounters] = {0, 0, 0, 0, 0, 0};
+    unsigned long long tot[kNumCounters] = {};
     for (int sl = 0; sl < kCounterSlots; ++sl)
         for (int k = 0; k < kNumCounters; ++k) tot[k] += c->h_counters[(size_t)sl * kCounterStride + k];
     c->stats.events = (int64_t)tot[0];

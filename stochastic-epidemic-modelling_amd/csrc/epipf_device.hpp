@@ -70,11 +70,25 @@ __device__ __forceinline__ double one_minus_u01(uint32_t lo, uint32_t hi) {
     return fma((double)ml, -0x1.0p-53, fma((double)mh, -0x1.0p-21, 1.0));
 }
 
+// ------------------------------------------------------------------------------- index checks
+// An ancestor / path index outside [0, n) would mean a search or indexing bug.  The release build clamps it (a
+// wrong answer the parity tests catch, never an out-of-bounds access); the debug build (make debug,
+// libepipf_debug.so) traps on it instead, so the fault is reported at the kernel that produced it.
+__device__ __forceinline__ int checked_index(int i, int n) {
+#ifdef EPIPF_DEBUG
+    if ((unsigned)i >= (unsigned)n) __builtin_trap();
+    return i;
+#else
+    return min(max(i, 0), n - 1);
+#endif
+}
+
 // ------------------------------------------------------------------------------- per-chain parameters
 struct ChainParam {
     double theta[kMaxTheta];   // SIR: beta,gamma  SEIR: beta,alpha,gamma  groups: beta[G][G], gamma
     double probs;              // binomial p, or normal noise ratio
-    double logp, log1mp;       // log(p), log1p(-p)  (host glibc, identical to the oracle's)
+    double logp, log1mp;       // log(p), log1p(-p): hi parts of their binary128 values (logfact.cpp)
+    double logp_lo, log1mp_lo; //   and the lo parts (binom_logpmf)
     uint32_t k0, k1;           // Philox key
     uint32_t f;                // filter index
     uint32_t flags;            // kChainFastSsa: the certified f32 event loop may run (EPIPF_SSA_FAST=0 clears it)
@@ -827,21 +841,76 @@ struct Shape {
 };
 
 // ------------------------------------------------------------------------------- observation weights
-// scipy binom.pmf(k, n, p) restated with a host-built log-factorial table lf[n] = lgamma(n + 1),
-// pmcmc.py:179.  Identical expression order to oracle/epipf_oracle.c:binom_pmf.
-__device__ __forceinline__ double binom_pmf(double k, double n, const ChainParam& cp, const double* lf,
-                                            int lf_max) {
+// scipy binom.pmf(k, n, p), pmcmc.py:179, evaluated as the log of its closed form
+//   L = (log n! - log k! - log (n-k)!) + (k log p + (n-k) log1p(-p))
+// carried as an unevaluated sum hi + lo: the log-factorials (lf: hi, lo pairs) and log p / log1p(-p) come from
+// binary128 on the host (logfact.cpp), the roundings of the hi parts are recovered exactly (two_sum, fma) and the
+// tiny lo terms summed in plain double.  |L - (hi + lo)| stays below ~1e-25 |L|-scale, so the weight
+// exp(hi) (1 + lo) is the true pmf to within exp's own rounding and one multiply-add -- scipy's Boost evaluation
+// is itself only good to ~1e-12 relative at these n, the restatement is not the limiting error.
+// Same operations as oracle/epipf_oracle.c:binom_logpmf.
+struct LogW {
+    double hi, lo;   // hi = -inf: pmf 0; NaN: bad p (scipy returns nan)
+};
+
+__device__ __forceinline__ void two_sum(double a, double b, double& s, double& e) {
+    s = a + b;
+    const double bb = s - a;
+    e = (a - (s - bb)) + (b - bb);
+}
+
+// plain-double log pmf from the hi parts only (the candidate ranking of particle_weight); -inf / NaN as LogW.hi
+__device__ __forceinline__ double binom_logpmf_hi(double k, double n, const ChainParam& cp, const double2* lf,
+                                                  int lf_max) {
     const double p = cp.probs;
     if (!(p >= 0.0 && p <= 1.0)) return __builtin_nan("");
-    if (k < 0.0 || k > n || k != floor(k)) return 0.0;
-    if (p == 0.0) return (k == 0.0) ? 1.0 : 0.0;
-    if (p == 1.0) return (k == n) ? 1.0 : 0.0;
+    if (k < 0.0 || k > n || k != floor(k)) return -__builtin_inf();
+    if (p == 0.0) return (k == 0.0) ? 0.0 : -__builtin_inf();
+    if (p == 1.0) return (k == n) ? 0.0 : -__builtin_inf();
     const int ni = min(max((int)n, 0), lf_max), ki = min(max((int)k, 0), lf_max);
-    double a = lf[ni] - lf[ki];
-    a = a - lf[min(max(ni - ki, 0), lf_max)];
-    const double b = k * cp.logp;
-    const double c = (n - k) * cp.log1mp;
-    return exp(a + (b + c));
+    const double a = (lf[ni].x - lf[ki].x) - lf[min(max(ni - ki, 0), lf_max)].x;
+    return a + (k * cp.logp + (n - k) * cp.log1mp);
+}
+
+// the compensated log pmf; the special cases as binom_logpmf_hi (lo = 0 there)
+__device__ __forceinline__ LogW binom_logpmf(double k, double n, const ChainParam& cp, const double2* lf, int lf_max) {
+    const double p = cp.probs;
+    if (!(p >= 0.0 && p <= 1.0)) return LogW{__builtin_nan(""), 0.0};
+    if (k < 0.0 || k > n || k != floor(k)) return LogW{-__builtin_inf(), 0.0};
+    if (p == 0.0) return LogW{(k == 0.0) ? 0.0 : -__builtin_inf(), 0.0};
+    if (p == 1.0) return LogW{(k == n) ? 0.0 : -__builtin_inf(), 0.0};
+    const int ni = min(max((int)n, 0), lf_max), ki = min(max((int)k, 0), lf_max);
+    const double2 fn = lf[ni], fk = lf[ki], fm = lf[min(max(ni - ki, 0), lf_max)];
+    const double m = n - k;
+    double s1, e1, s2, e2, s3, e3, s4, e4;
+    two_sum(fn.x, -fk.x, s1, e1);
+    two_sum(s1, -fm.x, s2, e2);
+    const double p1 = k * cp.logp, f1 = fma(k, cp.logp, -p1);       // exact products: p + f = k * logp
+    const double p2 = m * cp.log1mp, f2 = fma(m, cp.log1mp, -p2);
+    two_sum(p1, p2, s3, e3);
+    two_sum(s2, s3, s4, e4);
+    double lo = (fn.y - fk.y) - fm.y;
+    lo = lo + ((e1 + e2) + (e3 + e4));
+    lo = lo + (f1 + f2);
+    lo = lo + (k * cp.logp_lo + m * cp.log1mp_lo);
+    return LogW{s4, lo};
+}
+
+// sum of the magnitudes of binom_logpmf_hi's terms (+1): its result is within ~8 ulps of this (8 roundings, each
+// at most half an ulp of a partial sum bounded by it)
+__device__ __forceinline__ double logw_scale(double k, double n, const ChainParam& cp, const double2* lf, int lf_max) {
+    const int ni = min(max((int)n, 0), lf_max);
+    return (2.0 * fabs(lf[ni].x) + fabs(k * cp.logp)) + (fabs((n - k) * cp.log1mp) + 1.0);
+}
+
+// a < b for compensated logs of nearby size (hi - hi is exact within a factor 2, Sterbenz); -inf and NaN by hi
+__device__ __forceinline__ bool logw_less(const LogW& a, const LogW& b) {
+    if (a.hi != b.hi) {
+        const double d = a.hi - b.hi;
+        if (!(fabs(d) < 1.0)) return a.hi < b.hi;          // far apart (or infinite): the hi parts decide
+        return d + (a.lo - b.lo) < 0.0;
+    }
+    return a.lo < b.lo;
 }
 
 // scipy norm.pdf(y, loc=x, scale=probs*x+1e-4), pmcmc.py:181
@@ -852,43 +921,79 @@ __device__ __forceinline__ double normal_pdf(double y, double x, double probs) {
     return (exp(-(z * z) / 2.0) / 2.5066282746310002) / scale;
 }
 
-// log of binom_pmf with the same expression order: -inf for pmf 0, 0 for pmf 1, NaN for bad p
-__device__ __forceinline__ double binom_logpmf(double k, double n, const ChainParam& cp, const double* lf, int lf_max) {
-    const double p = cp.probs;
-    if (!(p >= 0.0 && p <= 1.0)) return __builtin_nan("");
-    if (k < 0.0 || k > n || k != floor(k)) return -__builtin_inf();
-    if (p == 0.0) return (k == 0.0) ? 0.0 : -__builtin_inf();
-    if (p == 1.0) return (k == n) ? 0.0 : -__builtin_inf();
-    const int ni = min(max((int)n, 0), lf_max), ki = min(max((int)k, 0), lf_max);
-    double a = lf[ni] - lf[ki];
-    a = a - lf[min(max(ni - ki, 0), lf_max)];
-    const double b = k * cp.logp;
-    const double c = (n - k) * cp.log1mp;
-    return a + (b + c);
+template <int MODEL, int G>
+__device__ __forceinline__ double observed(const double* x, int i) {
+    if constexpr (MODEL == kSubgroups2) {
+        double xo = 0.0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) xo = xo + x[3 * g + i];          // group sum, pmcmc.py:173,229
+        return xo;
+    } else {
+        return x[i];
+    }
 }
 
-// min over the K observed columns (np.min propagates NaN), pmcmc.py:178-181.  Binomial: exp is monotone, so
-// min_i exp(L_i) = exp(min_i L_i) -- one exp per particle instead of K, same value.
+// min over the K observed columns (np.min propagates NaN), pmcmc.py:178-181.  Binomial: exp is monotone, so the
+// minimum is taken on the logs and exponentiated once.  The columns are ranked on their plain-double logs; only
+// the smallest is evaluated compensated -- unless another column lies within the plain logs' error of it (a
+// near tie, wave-uniform branch: rare), when every column is, and the compensated logs decide.  The plain log's
+// error is a few ulps of log n! (<= 2^-48 |lf_hi[n]| with margin), so outside a near tie the ranking is exact.
 template <int MODEL, int G, int OBS>
 __device__ __forceinline__ double particle_weight(const double* x, const double* yrow, const ChainParam& cp,
-                                                  const double* lf, int lf_max) {
+                                                  const double2* lf, int lf_max) {
     constexpr int K = Shape<MODEL, G>::K;
-    double w = 0.0;
+    if constexpr (OBS == kNormal) {
+        double w = 0.0;
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
-        double xo;
-        if constexpr (MODEL == kSubgroups2) {
-            xo = 0.0;
-#pragma unroll
-            for (int g = 0; g < G; ++g) xo = xo + x[3 * g + i];       // group sum, pmcmc.py:173,229
-        } else {
-            xo = x[i];
+        for (int i = 0; i < K; ++i) {
+            const double wi = normal_pdf(yrow[i], observed<MODEL, G>(x, i), cp.probs);
+            if (i == 0 || isnan(wi)) w = wi;
+            else if (!isnan(w) && wi < w) w = wi;
         }
-        const double wi = (OBS == kBinomial) ? binom_logpmf(yrow[i], xo, cp, lf, lf_max) : normal_pdf(yrow[i], xo, cp.probs);
-        if (i == 0 || isnan(wi)) w = wi;
-        else if (!isnan(w) && wi < w) w = wi;
+        return w;
+    } else {
+        double lh[K], xo[K];
+        double m = 0.0;
+        int am = 0;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            xo[i] = observed<MODEL, G>(x, i);
+            lh[i] = binom_logpmf_hi(yrow[i], xo[i], cp, lf, lf_max);
+            if (i == 0 || isnan(lh[i])) { m = lh[i]; am = i; }
+            else if (!isnan(m) && lh[i] < m) { m = lh[i]; am = i; }
+        }
+        if (isnan(m)) return m;
+        // the minimum's operands, selected without indexing (registers)
+        double ys = yrow[0], xs = xo[0];
+#pragma unroll
+        for (int i = 1; i < K; ++i) {
+            ys = (am == i) ? yrow[i] : ys;
+            xs = (am == i) ? xo[i] : xs;
+        }
+        bool tie = false;
+        if (m > -__builtin_inf()) {
+            const double sm = logw_scale(ys, xs, cp, lf, lf_max);
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                if (i == am || (yrow[i] == ys && xo[i] == xs)) continue;     // identical operands: identical value
+                const double tol = (sm + logw_scale(yrow[i], xo[i], cp, lf, lf_max)) * 0x1.0p-46;
+                tie = tie || (lh[i] - m <= tol);
+            }
+        }
+        LogW L;
+        if (tie) {
+            L = binom_logpmf(yrow[0], xo[0], cp, lf, lf_max);
+#pragma unroll
+            for (int i = 1; i < K; ++i) {
+                const LogW li = binom_logpmf(yrow[i], xo[i], cp, lf, lf_max);
+                if (logw_less(li, L)) L = li;
+            }
+        } else {
+            L = binom_logpmf(ys, xs, cp, lf, lf_max);
+        }
+        const double e = exp(L.hi);
+        return fma(e, L.lo, e);                                        // exp(hi + lo) = exp(hi) (1 + lo)
     }
-    return (OBS == kBinomial) ? exp(w) : w;
 }
 
 // ------------------------------------------------------------------------------- block scan (doubles)
@@ -926,6 +1031,14 @@ __device__ __forceinline__ double block_inclusive_scan(double x, double* lds) {
 // Draws that fail the test are resolved exactly by resample_exact_wave.
 __device__ __forceinline__ double cert_halfwidth(int i, double v, double cert_k) {
     return ((double)i + cert_k) * 0x1.00001p-53 * v;
+}
+
+// The reference's own CDF is numpy's over scipy's weights, which differ from the device's by at most E relative
+// each (E: scipy's error envelope plus the device's).  Then |cdf_ref_i - cdf_i| <= 2E v (1 - v)
+// (1 + tiny), and ref_k = 2E (1 + 2^-10).  A draw whose U lies within delta_i + that of a boundary of its answer
+// may differ from the reference's: counted (resample_ref_ambiguous), never changed.
+__device__ __forceinline__ double ref_halfwidth(double v, double ref_k) {
+    return ref_k * (v * (1.0 - v));
 }
 
 // Two-level search of v (bpex: exclusive prefix of the block sums and bsum: block sums, both in LDS;
@@ -971,7 +1084,7 @@ __device__ __forceinline__ int inblock_search(double base, const double* __restr
 template <int WG, bool FLAT = false>
 __device__ __forceinline__ int resample_search(double U, const double* bpex, const double* bsum, int B,
                                                double total, const double* wloc, int N, double cert_k,
-                                               bool& certified) {
+                                               bool& certified, double ref_k, bool& ambiguous) {
     const double Ut = U * total;
     int lo = 0, hi = B - 1;
     while (lo < hi) {
@@ -988,6 +1101,8 @@ __device__ __forceinline__ int resample_search(double U, const double* bpex, con
                               : (b > 0 ? (bpex[b - 1] + bsum[b - 1]) / total : -1.0);
     certified = (va - cert_halfwidth(a, va, cert_k) > U) &&
                 (a == 0 || vp + cert_halfwidth(a - 1, vp, cert_k) < U) && a < N;
+    ambiguous = !((va - (cert_halfwidth(a, va, cert_k) + ref_halfwidth(va, ref_k)) > U) &&
+                  (a == 0 || vp + (cert_halfwidth(a - 1, vp, cert_k) + ref_halfwidth(vp, ref_k)) < U));
     return a;
 }
 
@@ -999,7 +1114,7 @@ template <bool FLAT = false>
 __device__ __forceinline__ int resample_search_seg(double U, const double* seg_start, const double* seg_end, int nseg,
                                                    int S, const double* __restrict__ bsum_g, int B, double total,
                                                    const double* __restrict__ wloc, int WGB, int N, double cert_k,
-                                                   bool& certified) {
+                                                   bool& certified, double ref_k, bool& ambiguous) {
     const double Ut = U * total;                                        // search on U * total (resample_search)
     int lo = 0, hi = nseg - 1;
     while (lo < hi) {
@@ -1037,6 +1152,8 @@ __device__ __forceinline__ int resample_search_seg(double U, const double* seg_s
     const double vp = (l > 0) ? (base + L[l - 1]) / total : (b > 0 ? pb / total : -1.0);
     certified = (va - cert_halfwidth(a, va, cert_k) > U) &&
                 (a == 0 || vp + cert_halfwidth(a - 1, vp, cert_k) < U) && a < N;
+    ambiguous = !((va - (cert_halfwidth(a, va, cert_k) + ref_halfwidth(va, ref_k)) > U) &&
+                  (a == 0 || vp + (cert_halfwidth(a - 1, vp, cert_k) + ref_halfwidth(vp, ref_k)) < U));
     return a;
 }
 
@@ -1089,7 +1206,8 @@ struct ChunkStream {
     }
 };
 
-__device__ __forceinline__ int resample_exact_wave(bool need, double U, const double* __restrict__ w, int N) {
+__device__ __forceinline__ int resample_exact_wave(bool need, double U, const double* __restrict__ w, int N,
+                                                   double ref_k, bool& ambiguous) {
     ChunkStream cs;
     // pass 1: S
     double S = 0.0;
@@ -1125,16 +1243,25 @@ __device__ __forceinline__ int resample_exact_wave(bool need, double U, const do
     bool waiting = need;
     ExactTarget tg = exact_next_target(waiting, U);
     c = 0.0;
+    double cprev = 0.0;
     cs.start(w, N);
 #pragma unroll 1
     for (int cb = 0; cb < N && !tg.done; cb += 64) {
         const double q = cs.next(cb) / S;
         const int n = min(64, N - cb);
         for (int l = 0; l < n; ++l) {
+            cprev = c;
             c = c + readlane_f64(q, l);
             const double r = c * rl;
             while (!tg.done && r > tg.lo && (r > tg.hi || c / last > tg.U)) {   // cdf_i > U*: lanes at U* done
-                if (waiting && U == tg.U) { ans = cb + l; waiting = false; }
+                if (waiting && U == tg.U) {
+                    ans = cb + l;
+                    waiting = false;
+                    // cdf_{i-1} <= U < cdf_i exactly; the reference's boundaries are within ref_halfwidth of them
+                    const double ci = c / last, cp = cprev / last;
+                    ambiguous = (ci - U <= ref_halfwidth(ci, ref_k)) ||
+                                (cb + l > 0 && U - cp <= ref_halfwidth(cp, ref_k));
+                }
                 tg = exact_next_target(waiting, U);
             }
             if (tg.done) break;

@@ -291,7 +291,7 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
                 a.log_zeta[(size_t)chain * a.T + p] = a.log_zeta[(size_t)chain * a.T + p - 1] + log(total / (double)a.N);
             double U = 0.0;
             int anc = 0;
-            bool certified = true;
+            bool certified = true, ambiguous = false;
             if (j < a.N) {                               // pmcmc.py:188-190
                 const uint32_t rtag = ((uint32_t)p & 0xFFFFFFu) | kDomainResample;
                 if (a.resample_mode == 0) {
@@ -303,20 +303,21 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
                 }
                 if (a.seg == 1)
                     anc = resample_search<64, true>(U, seg_start + a.B, seg_start, a.B, total, a.wloc + wprev, a.N, a.cert_k,
-                                              certified);
+                                              certified, a.ref_k, ambiguous);
                 else
                     anc = resample_search_seg<true>(U, seg_start, seg_end, a.nseg, a.seg, a.bsum + bprev, a.B, total,
-                                              a.wloc + wprev, 64, a.N, a.cert_k, certified);
+                                              a.wloc + wprev, 64, a.N, a.cert_k, certified, a.ref_k, ambiguous);
             }
             if (__any(!certified)) {
-                const int e = resample_exact_wave(!certified, U, a.wraw + wprev, a.N);
+                const int e = resample_exact_wave(!certified, U, a.wraw + wprev, a.N, a.ref_k, ambiguous);
                 if (!certified) {
                     anc = e;
                     atomicAdd(counter_slot(a.counters) + 1, 1ull);
                 }
             }
+            if (ambiguous) atomicAdd(counter_slot(a.counters) + 6, 1ull);
             if (j < a.N) {                               // :193-199
-                anc = min(max(anc, 0), a.N - 1);
+                anc = checked_index(anc, a.N);
                 a.ancestry[(size_t)chain * a.anc_stride + (size_t)p * a.N + j] = anc;
                 const int32_t* hp = a.hidden + (size_t)chain * a.hist_stride + ((size_t)(p - 1) * a.N + anc) * C;
 #pragma unroll

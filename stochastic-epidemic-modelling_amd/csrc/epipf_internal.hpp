@@ -5,13 +5,24 @@
 
 #include "epipf_device.hpp"
 
+// roctx ranges (the debug build, EPIPF_ROCTX): one around each epipf_run (an MH iteration's filter) and one around
+// the enqueue of each filter step, so a rocprofv3 --marker-trace timeline shows which host call a kernel belongs to
+#ifdef EPIPF_ROCTX
+#include <rocprofiler-sdk-roctx/roctx.h>
+#define EPIPF_RANGE_PUSH(msg) roctxRangePushA(msg)
+#define EPIPF_RANGE_POP() roctxRangePop()
+#else
+#define EPIPF_RANGE_PUSH(msg) ((void)0)
+#define EPIPF_RANGE_POP() ((void)0)
+#endif
+
 namespace epipf {
 
 // Device counters are spread over kCounterSlots cache lines: same-address atomics from every wave serialise
 // (~10 ns each on MI355X), which at 5k waves per launch cost more than the launch itself.
 constexpr int kCounterSlots = 64;
 constexpr int kCounterStride = 16;   // u64 per slot = 128 B
-constexpr int kNumCounters = 6;
+constexpr int kNumCounters = 7;
 
 __device__ __forceinline__ unsigned long long* counter_slot(unsigned long long* base) {
     return base + (size_t)((blockIdx.x + 7u * blockIdx.y) & (kCounterSlots - 1)) * kCounterStride;
@@ -24,7 +35,7 @@ __device__ __forceinline__ unsigned long long* counter_slot(unsigned long long* 
 //   wloc     f64   [2][max_chains][B*WG]          in-block inclusive prefix of wraw
 //   bsum     f64   [2][max_chains][B]             block totals
 //   log_zeta f64   [max_chains][T]
-//   Y        f64   [T][K];  lf f64 [lf_max+1] = lgamma(n+1)
+//   Y        f64   [T][K];  lf f64x2 [lf_max+1] = log n! as hi + lo (binary128 on the host, logfact.cpp)
 struct StepArgs {
     int N, T, B, wg, max_chains, resample_mode, count_events, lf_max;
     int chain0;                   // first chain of this launch (chain groups run on separate streams)
@@ -34,8 +45,9 @@ struct StepArgs {
     int seg, nseg;                // block-sum prefix: S blocks per segment, ceil(B / S) segments (<= kMaxSegments)
     size_t hist_stride, anc_stride, wstride, bstride;
     double cert_k;                // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp)
+    double ref_k;                 // 2E (1 + 2^-10): reference-ambiguity bracket (ref_halfwidth)
     const double* Y;
-    const double* lf;
+    const double2* lf;            // (hi, lo) of log n!, n = 0..lf_max (binom_logpmf)
     const LogTab* logtab;         // glibc log table [kLogTabEntries] (context-resident)
     const ChainParam* cp;
     int32_t* hidden;
@@ -47,7 +59,8 @@ struct StepArgs {
     int32_t* status;
     unsigned long long* counters;  // [kCounterSlots][kCounterStride]: [0] events, [1] resample fallbacks,
                                    // [2] SSA lane-iterations, [3] wave-iterations x 64, [4] particle-steps on
-                                   // the exact SSA loop, [5] waves with one (summed on the host)
+                                   // the exact SSA loop, [5] waves with one, [6] reference-ambiguous draws
+                                   // (summed on the host)
     double npop[kMaxG], mu[kMaxG], emu[kMaxG];
     int kmax[kMaxG];
 };
@@ -151,6 +164,10 @@ struct FilterStreams {
     hipEvent_t ev_init, ev_step0, ev_end;   // timing (profiling on) or null
     hipEvent_t g_begin[kMaxFilterStreams], g_end[kMaxFilterStreams];   // per-group step-kernel span, or null
 };
+
+// logfact.cpp (host, binary128): log n! and log p / log1p(-p) split into hi + lo doubles
+void logfact_table(int n_max, double* out);
+void log_p_split(double p, double* logp_hi, double* logp_lo, double* log1mp_hi, double* log1mp_lo);
 
 size_t step_lds_bytes(int B, int wg);
 // lane-group step kernel (epipf_group.hip): W lanes per particle, launched as grid (B, chains) x 64 W threads

@@ -15,6 +15,8 @@
 #include "epipf_step.hpp"
 #include <algorithm>
 
+#include <cstdio>
+
 #include "epipf_internal.hpp"
 
 #ifndef EPIPF_STEP_WAVES
@@ -108,7 +110,7 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
     // (d) multinomial (or systematic) draw and certified search, pmcmc.py:188-190
     double U = 0.0;
     int anc = 0;
-    bool certified = true;
+    bool certified = true, ambiguous = false;
     if (j < a.N) {
         const uint32_t rtag = ((uint32_t)p & 0xFFFFFFu) | kDomainResample;
         if (a.resample_mode == 0) {
@@ -120,18 +122,19 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
         }
         if (a.seg == 1)
             anc = resample_search<WG>(U, seg_start + a.B, seg_start, a.B, total, a.wloc + wprev, a.N, a.cert_k,
-                                      certified);
+                                      certified, a.ref_k, ambiguous);
         else
             anc = resample_search_seg(U, seg_start, seg_end, a.nseg, a.seg, a.bsum + bprev, a.B, total,
-                                      a.wloc + wprev, WG, a.N, a.cert_k, certified);
+                                      a.wloc + wprev, WG, a.N, a.cert_k, certified, a.ref_k, ambiguous);
     }
     if (__any(!certified)) {   // wave-uniform: the whole wave resolves its uncertified draws exactly
-        const int e = resample_exact_wave(!certified, U, a.wraw + wprev, a.N);
+        const int e = resample_exact_wave(!certified, U, a.wraw + wprev, a.N, a.ref_k, ambiguous);
         if (!certified) {
             anc = e;
             atomicAdd(counter_slot(a.counters) + 1, 1ull);
         }
     }
+    if (ambiguous) atomicAdd(counter_slot(a.counters) + 6, 1ull);   // rare (~1e-8 of draws at config 2)
     // (f) gather the parent state, (g) propagate over [0, 1], :195-220: the certified f32 loop, then the exact path
     // for the lanes it hands back.  The exact path's log table is copied to LDS only by waves that need it (~1% at
     // config 2): one wave per block, so the wave-uniform test is block-uniform and the barriers are legal.
@@ -141,7 +144,7 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
     const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
     bool fast_ok = false, eligible = false;
     if (j < a.N) {
-        anc = min(max(anc, 0), a.N - 1);
+        anc = checked_index(anc, a.N);
         a.ancestry[(size_t)chain * a.anc_stride + (size_t)p * a.N + j] = anc;   // :193
         const int32_t* hp = a.hidden + (size_t)chain * a.hist_stride + ((size_t)(p - 1) * a.N + anc) * C;
 #pragma unroll
@@ -219,13 +222,13 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
 __global__ void path_sample_kernel(PathArgs a) {
     const int chain = blockIdx.x * blockDim.x + threadIdx.x;
     if (chain >= a.n_chains) return;
-    int chosen = min(max(a.chosen[chain], 0), a.N - 1);
+    int chosen = checked_index(a.chosen[chain], a.N);
     const int32_t* hid = a.hidden + (size_t)chain * a.hist_stride;
     const int32_t* anc = a.ancestry + (size_t)chain * a.anc_stride;
     int32_t* out = a.traj + (size_t)chain * a.T * a.C;
     for (int c = 0; c < a.C; ++c) out[(size_t)(a.T - 1) * a.C + c] = hid[((size_t)(a.T - 1) * a.N + chosen) * a.C + c];
     for (int p = a.T - 2; p >= 0; --p) {
-        chosen = min(max(anc[(size_t)p * a.N + chosen], 0), a.N - 1);     // ancestry[p], as the reference
+        chosen = checked_index(anc[(size_t)p * a.N + chosen], a.N);       // ancestry[p], as the reference
         for (int c = 0; c < a.C; ++c) out[(size_t)p * a.C + c] = hid[((size_t)p * a.N + chosen) * a.C + c];
     }
 }
@@ -322,17 +325,17 @@ __global__ __launch_bounds__(WG) void resample_search_kernel(ResampleArgs a) {
         return;
     }
     const double U = (j < a.N) ? a.u[j] : 0.0;
-    bool certified = true;
+    bool certified = true, ambiguous = false;      // standalone resampler: no reference weights, ref_k = 0
     int anc = 0;
-    if (j < a.N) anc = resample_search<WG>(U, bpex, bsum, a.B, total, a.wloc, a.N, a.cert_k, certified);
+    if (j < a.N) anc = resample_search<WG>(U, bpex, bsum, a.B, total, a.wloc, a.N, a.cert_k, certified, 0.0, ambiguous);
     if (__any(!certified)) {
-        const int e = resample_exact_wave(!certified, U, a.wraw, a.N);
+        const int e = resample_exact_wave(!certified, U, a.wraw, a.N, 0.0, ambiguous);
         if (!certified) {
             anc = e;
             atomicAdd(a.fallbacks, 1ull);
         }
     }
-    if (j < a.N) a.out[j] = min(max(anc, 0), a.N - 1);
+    if (j < a.N) a.out[j] = checked_index(anc, a.N);
 }
 
 // ------------------------------------------------------------------------------- launchers
@@ -377,8 +380,14 @@ static hipError_t launch_filter_t(const StepArgs& a, int n_chains, const FilterS
         if (g == 0 && fs.ev_step0) (void)hipEventRecord(fs.ev_step0, s);
         if (fs.g_begin[g]) (void)hipEventRecord(fs.g_begin[g], s);
         for (int p = 1; p < a.T; ++p) {
+#ifdef EPIPF_ROCTX
+            char msg[48];
+            snprintf(msg, sizeof msg, "filter step %d group %d", p, g);
+            EPIPF_RANGE_PUSH(msg);
+#endif
             if (group) group(ag, p, grid, glds, s);
             else hipLaunchKernelGGL((pf_step_kernel<MODEL, G, OBS, WG>), grid, block, lds, s, ag, p);
+            EPIPF_RANGE_POP();
         }
         if (fs.g_end[g]) (void)hipEventRecord(fs.g_end[g], s);
         if (g > 0) (void)hipEventRecord(fs.join[g], s);

@@ -1,0 +1,52 @@
+// logfact.cpp -- host tables for the compensated binomial weight (epipf_device.hpp: binom_logpmf).
+//
+// The reference's weight is scipy.stats.binom.pmf (pmcmc.py:179).  The device evaluates
+//   log pmf = (log n! - log k! - log (n-k)!) + (k log p + (n-k) log1p(-p))
+// as an unevaluated sum hi + lo of doubles, from log-factorials and log p / log1p(-p) rounded from binary128
+// (libquadmath) to a hi double plus a lo double.  The table carries ~106 significant bits, so the weight's
+// only rounding errors left are exp's and one multiply-add.
+// Built with g++ (binary128 is a host type; nothing here runs on the GPU).
+#include <quadmath.h>
+
+#include <algorithm>
+#include <cmath>
+#include <thread>
+#include <vector>
+
+namespace {
+
+inline void split(__float128 q, double* hi, double* lo) {
+    const double h = (double)q;
+    *hi = h;
+    *lo = std::isfinite(h) ? (double)(q - (__float128)h) : 0.0;
+}
+
+void fill(int from, int to, double* out) {
+    for (int n = from; n < to; ++n) split(lgammaq((__float128)n + 1), &out[2 * (size_t)n], &out[2 * (size_t)n + 1]);
+}
+
+}  // namespace
+
+namespace epipf {
+
+// out[2n], out[2n+1] = hi, lo of log(n!) for n = 0..n_max (lgammaq: ~2 us per entry, threaded above 64k entries)
+void logfact_table(int n_max, double* out) {
+    const int n = n_max + 1;
+    const int threads = n > 65536 ? (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1;
+    if (threads == 1) {
+        fill(0, n, out);
+        return;
+    }
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads; ++t)
+        pool.emplace_back(fill, (int)((long)n * t / threads), (int)((long)n * (t + 1) / threads), out);
+    for (auto& th : pool) th.join();
+}
+
+// hi/lo of log(p) and log1p(-p) (the weight's per-chain constants)
+void log_p_split(double p, double* logp_hi, double* logp_lo, double* log1mp_hi, double* log1mp_lo) {
+    split(logq((__float128)p), logp_hi, logp_lo);
+    split(log1pq(-(__float128)p), log1mp_hi, log1mp_lo);
+}
+
+}  // namespace epipf

@@ -16,12 +16,13 @@ SIR, SEIR, SIR_SUBGROUPS, SIR_SUBGROUPS2 = 0, 1, 2, 3
 OBS_BINOMIAL, OBS_NORMAL = 0, 1
 RESAMPLE_MULTINOMIAL, RESAMPLE_SYSTEMATIC = 0, 1
 PROFILE_OFF, PROFILE_TIMING, PROFILE_COUNTERS = 0, 1, 2
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 EXPORTS = (
     "epipf_create", "epipf_destroy", "epipf_set_observations", "epipf_set_population", "epipf_run",
     "epipf_copy_history", "epipf_path_sample", "epipf_simulate", "epipf_resample", "epipf_set_profiling",
     "epipf_get_stats", "epipf_reset_stats", "epipf_set_streams", "epipf_set_lanes", "epipf_last_error", "epipf_abi_version", "epipf_device_count",
+    "epipf_build_id",
     "epipf_abc", "epipf_abc_trials", "epipf_glibc_log", "epipf_simulate_path",
 )
 
@@ -47,6 +48,7 @@ class Stats(ctypes.Structure):
         ("step_kernel_launches", ctypes.c_int64),
         ("last_lanes", ctypes.c_int64),
         ("last_lane_events", ctypes.c_int64),
+        ("resample_ref_ambiguous", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -88,6 +90,7 @@ def load():
         "epipf_reset_stats": ([P], i32),
         "epipf_last_error": ([], ctypes.c_char_p),
         "epipf_abi_version": ([], i32),
+        "epipf_build_id": ([], ctypes.c_char_p),
         "epipf_device_count": ([], i32),
         "epipf_abc": ([P, P, i32, i32, f64, P, u64, u32, ctypes.c_int64, i32, P, P, P, P], i32),
         "epipf_abc_trials": ([P, P, i32, P, u64, u32, u32, i32, P, P, P, P], i32),
@@ -102,6 +105,11 @@ def load():
         raise EpipfError(f"libepipf.so ABI {L.epipf_abi_version()} != expected {ABI_VERSION}")
     _lib = L
     return L
+
+
+def build_id():
+    """The loaded library's build id (epipf_build_id: hash of its sources and flags)."""
+    return load().epipf_build_id().decode()
 
 
 def check(rc, what):

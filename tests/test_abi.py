@@ -63,3 +63,20 @@ def test_constants_match_header():
     assert int(defs["EPIPF_ABI_VERSION"]) == _lib.ABI_VERSION
     assert int(defs["EPIPF_PROFILE_TIMING"]) == _lib.PROFILE_TIMING
     assert int(defs["EPIPF_PROFILE_COUNTERS"]) == _lib.PROFILE_COUNTERS
+
+
+def test_build_id_is_a_source_hash():
+    from epipf import _lib
+    bid = _lib.build_id()
+    assert len(bid) == 16 and int(bid, 16) >= 0, bid
+
+
+def test_debug_library_exports_the_same_boundary():
+    """libepipf_debug.so (make debug: device traps, roctx ranges) is a drop-in for libepipf.so."""
+    path = os.path.join(PKG, "lib", "libepipf_debug.so")
+    assert os.path.exists(path), "run __graft_entry__.build() first"
+    D = ctypes.CDLL(path)
+    assert not [s for s in declared_symbols() if not hasattr(D, s)]
+    D.epipf_build_id.restype = ctypes.c_char_p
+    from epipf import _lib
+    assert D.epipf_build_id().decode() == _lib.build_id() + "-debug"

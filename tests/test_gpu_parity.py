@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 
 import oracle
+import reference_replay
 from conftest import case_args
 
 pytestmark = pytest.mark.gpu
@@ -560,21 +561,28 @@ def test_filter_short_horizons_and_extinct_starts_vs_oracle(datasets_golden, mod
     np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
 
 
-@pytest.mark.parametrize("cfg,chains,T", [(3, 2, None), (4, 2, None), (5, 2, None)])
-def test_full_size_baseline_configs_vs_oracle(cfg, chains, T):
+@pytest.mark.parametrize("cfg,chains,lanes,streams,checked", [
+    (3, 2, 0, None, None), (3, 2, 1, None, None),
+    (4, 2, 0, None, None), (4, 2, 1, None, None),
+    (5, 2, 0, None, None), (5, 2, 1, None, None),
+    # the bench's own layout: many chains on 4 chain-group streams, one lane per particle (pf_step_kernel, XCD-aware
+    # grid), a seeded subset of the chains checked -- the kernel that produces bench.py's config-3 / config-5 numbers
+    (3, 16, 1, 4, (0, 5, 10, 15)), (5, 16, 1, 4, (0, 6, 9, 15)),
+])
+def test_full_size_baseline_configs_vs_oracle(cfg, chains, lanes, streams, checked):
     """BASELINE configs 3 (SEIR, normal observations, N = 10^4, T = 200), 4 (SIR under-reported, N = 5*10^4, all 15
     rows: segmented block prefix) and 5 (2-group SIR, N = 10^4) at their full bench size, on the bench's own
-    dataset and starting theta plus a perturbed theta (one batched launch, one chain each): states and ancestors
-    bit-exact vs the oracle (pmcmc.py:123-233 restated), log-likelihoods within 1e-9 absolute."""
+    dataset and starting theta plus perturbed thetas (one batched launch, one chain each), on the automatic kernel
+    choice (lanes = 0: the lane-group kernel at 2 chains) and on the one-lane pf_step_kernel (lanes = 1): states and
+    ancestors bit-exact vs the oracle (pmcmc.py:123-233 restated), log-likelihoods within 1e-9 absolute."""
     from epipf import datasets
     from epipf.engine import Engine, model_id, theta_vector
     Y, meta = datasets.benchmark_dataset(cfg)
-    if T:
-        Y = Y[:T]
     N = meta["N"]
     mid = model_id(meta["model"])
     base = np.asarray(meta["theta"], dtype=np.float64)
-    thetas = np.stack([base * (1.0 + 0.07 * c * (-1) ** np.arange(base.size)) for c in range(chains)])
+    thetas = np.stack([base * (1.0 + 0.07 * (c % 5) * (-1) ** (np.arange(base.size) + c // 5))
+                       for c in range(chains)])
     if mid >= 2:
         G = int(round(np.sqrt(base.size - 1)))
         ref_th = [(t[:G * G].reshape(G, G), t[-1]) for t in thetas]
@@ -584,16 +592,36 @@ def test_full_size_baseline_configs_vs_oracle(cfg, chains, T):
     eng = Engine(meta["model"], G, N, Y.shape[0], chains)
     eng.set_observations(Y)
     eng.set_population(meta["n_population"], meta["mu"])
+    eng.set_lanes(lanes)
+    if streams:
+        eng.set_streams(streams)
     obs = bool(meta.get("observations", False))
     keys = [9000 + 17 * c for c in range(chains)]
     lz, st = eng.run(np.stack([theta_vector(mid, t)[0] for t in ref_th]), [meta["probs"]] * chains, keys,
                      [5 + c for c in range(chains)], observations=obs)
+    stats = eng.stats()
+    ran_lanes = stats["last_lanes"]
     hid, anc = eng.history(chains)
     eng.close()
-    for c in range(chains):
+    if lanes == 1:
+        assert ran_lanes == 1, "the one-lane kernel did not run"
+    elif cfg in (3, 5):
+        assert ran_lanes > 1, "expected the lane-group kernel at 2 chains"
+    draws = bad = 0
+    for c in (checked or range(chains)):
         o = oracle.particle_filter(Y, meta["model"], ref_th[c], obs, meta["probs"], N, meta["n_population"],
                                    meta["mu"], key=keys[c], filter_index=5 + c)
         assert int(st[c]) == o["status"] == 0, (c, st[c], o["status"])
         np.testing.assert_array_equal(hid[c], o["hidden"])
         np.testing.assert_array_equal(anc[c], o["ancestry"])
         np.testing.assert_allclose(lz[c], o["log_zetas"], rtol=1e-12, atol=1e-9)
+        # and against the reference itself: scipy's weights on these states, numpy's choice on the keyed uniforms
+        d, b = reference_replay.replay(Y, hid[c], anc[c], meta["model"], obs, meta["probs"], keys[c], 5 + c)
+        draws += d
+        bad += b
+    # reference-ambiguous draws (uniform within scipy's error envelope of a CDF boundary) are counted for every
+    # chain of the launch: expected ~0.67 E N per draw, i.e. well below one here
+    print(f"cfg {cfg} lanes {ran_lanes}: {draws} draws replayed against scipy, {bad} differ; "
+          f"{stats['resample_ref_ambiguous']} reference-ambiguous draws of {chains * N * (Y.shape[0] - 1)}")
+    assert bad == 0
+    assert stats["resample_ref_ambiguous"] <= 3
