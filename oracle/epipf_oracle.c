@@ -254,24 +254,30 @@ static double* logfact_table(int n_max) {
     for (int n = 0; n <= n_max; ++n) split128(lgammaq((__float128)n + 1), &t[2 * (size_t)n], &t[2 * (size_t)n + 1]);
     return t;
 }
+static void fast_two_sum(double a, double b, double* s, double* e) {   /* exact for |a| >= |b| */
+    *s = a + b;
+    *e = b - (*s - a);
+}
 static void two_sum(double a, double b, double* s, double* e) {
     *s = a + b;
     const double bb = *s - a;
     *e = (a - (*s - bb)) + (b - bb);
 }
-/* the regular case from the table entries (hi, lo) of log n!, log k!, log (n-k)! */
+/* the regular case from the table entries (hi, lo) of log n!, log k!, log (n-k)!: the factorial differences are
+ * fast two-sums (log n! >= log k!, log(n!/k!) >= log (n-k)!), the products' errors exact (fma), the products and
+ * the total exact two-sums, the lo terms summed in double -- the device's operations (binom_logpmf_plain / _core) */
 static logw_t binom_logpmf_entries(double k, double n, const logp_t* lp, const double* fn, const double* fk,
                                    const double* fm) {
     const double m = n - k;
     double s1, e1, s2, e2, s3, e3, s4, e4;
-    two_sum(fn[0], -fk[0], &s1, &e1);
-    two_sum(s1, -fm[0], &s2, &e2);
+    fast_two_sum(fn[0], -fk[0], &s1, &e1);
+    fast_two_sum(s1, -fm[0], &s2, &e2);
+    const double lt = ((fn[1] - fk[1]) - fm[1]) + (e1 + e2);
     const double p1 = k * lp->logp, f1 = fma(k, lp->logp, -p1);   /* exact products: p1 + f1 = k * logp */
     const double p2 = m * lp->log1mp, f2 = fma(m, lp->log1mp, -p2);
     two_sum(p1, p2, &s3, &e3);
     two_sum(s2, s3, &s4, &e4);
-    double lo = (fn[1] - fk[1]) - fm[1];
-    lo = lo + ((e1 + e2) + (e3 + e4));
+    double lo = lt + (e3 + e4);
     lo = lo + (f1 + f2);
     lo = lo + (k * lp->logp_lo + m * lp->log1mp_lo);
     logw_t r = {s4, lo};

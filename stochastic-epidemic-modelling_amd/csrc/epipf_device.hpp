@@ -89,6 +89,7 @@ struct ChainParam {
     double probs;              // binomial p, or normal noise ratio
     double logp, log1mp;       // log(p), log1p(-p): hi parts of their binary128 values (logfact.cpp)
     double logp_lo, log1mp_lo; //   and the lo parts (binom_logpmf)
+    double tie_tol;            // particle_weight: bound on the plain column logs' error (host, epipf_run)
     uint32_t k0, k1;           // Philox key
     uint32_t f;                // filter index
     uint32_t flags;            // kChainFastSsa: the certified f32 event loop may run (EPIPF_SSA_FAST=0 clears it)
@@ -859,48 +860,68 @@ __device__ __forceinline__ void two_sum(double a, double b, double& s, double& e
     e = (a - (s - bb)) + (b - bb);
 }
 
-// plain-double log pmf from the hi parts only (the candidate ranking of particle_weight); -inf / NaN as LogW.hi
-__device__ __forceinline__ double binom_logpmf_hi(double k, double n, const ChainParam& cp, const double2* lf,
-                                                  int lf_max) {
+// Dekker's fast two-sum: s + e = a + b exactly when |a| >= |b|
+__device__ __forceinline__ void fast_two_sum(double a, double b, double& s, double& e) {
+    s = a + b;
+    e = b - (s - a);
+}
+
+// The log-factorial table: lf[n] = hi and lf[lf_max + 1 + n] = lo of log n!, n = 0..lf_max (binary128 split on the
+// host, logfact.cpp).  Hi and lo apart: the ranking pass reads only the hi parts (the table footprint in L1/L2 of
+// the old plain weight), and the lo parts of the minimum's three entries are read once it is known.
+struct LfIdx { int n, k, m; };
+
+// Plain-double log pmf from the hi parts (the candidate ranking of particle_weight; -inf / NaN as LogW.hi), plus
+// what the compensated value needs: s2 = (log n! - log k!) - log (n-k)! in hi parts (the plain sum's own first two
+// additions), e12 = those two additions' exact rounding errors, and the entries' indices.  log n! >= log k! and
+// log(n!/k!) >= log (n-k)! (n!/k! is a product of n-k factors each >= its counterpart in (n-k)!), so both are fast
+// two-sums.
+__device__ __forceinline__ double binom_logpmf_plain(double k, double n, const ChainParam& cp, const double* lf,
+                                                     int lf_max, double& s2, double& e12, LfIdx& ix) {
+    s2 = e12 = 0.0;
+    ix = LfIdx{0, 0, 0};
     const double p = cp.probs;
     if (!(p >= 0.0 && p <= 1.0)) return __builtin_nan("");
     if (k < 0.0 || k > n || k != floor(k)) return -__builtin_inf();
     if (p == 0.0) return (k == 0.0) ? 0.0 : -__builtin_inf();
     if (p == 1.0) return (k == n) ? 0.0 : -__builtin_inf();
     const int ni = min(max((int)n, 0), lf_max), ki = min(max((int)k, 0), lf_max);
-    const double a = (lf[ni].x - lf[ki].x) - lf[min(max(ni - ki, 0), lf_max)].x;
-    return a + (k * cp.logp + (n - k) * cp.log1mp);
+    ix = LfIdx{ni, ki, min(max(ni - ki, 0), lf_max)};
+    double s1, e1, e2;
+    fast_two_sum(lf[ix.n], -lf[ix.k], s1, e1);
+    fast_two_sum(s1, -lf[ix.m], s2, e2);
+    e12 = e1 + e2;
+    return s2 + (k * cp.logp + (n - k) * cp.log1mp);
 }
 
-// the compensated log pmf; the special cases as binom_logpmf_hi (lo = 0 there)
-__device__ __forceinline__ LogW binom_logpmf(double k, double n, const ChainParam& cp, const double2* lf, int lf_max) {
-    const double p = cp.probs;
-    if (!(p >= 0.0 && p <= 1.0)) return LogW{__builtin_nan(""), 0.0};
-    if (k < 0.0 || k > n || k != floor(k)) return LogW{-__builtin_inf(), 0.0};
-    if (p == 0.0) return LogW{(k == 0.0) ? 0.0 : -__builtin_inf(), 0.0};
-    if (p == 1.0) return LogW{(k == n) ? 0.0 : -__builtin_inf(), 0.0};
-    const int ni = min(max((int)n, 0), lf_max), ki = min(max((int)k, 0), lf_max);
-    const double2 fn = lf[ni], fk = lf[ki], fm = lf[min(max(ni - ki, 0), lf_max)];
+// The compensated log pmf of a regular case (0 < p < 1, k integral in [0, n]) from binom_logpmf_plain's outputs:
+// the table's lo parts, the products' exact errors (fma), an exact two-sum of the products and one of the total, the
+// lo terms summed in double.
+__device__ __forceinline__ LogW binom_logpmf_core(double k, double n, double s2, double e12, LfIdx ix,
+                                                  const double* lf, int lf_max, double logp, double log1mp,
+                                                  double logp_lo, double log1mp_lo) {
+    const double* lo_tab = lf + lf_max + 1;
+    const double lt = ((lo_tab[ix.n] - lo_tab[ix.k]) - lo_tab[ix.m]) + e12;
     const double m = n - k;
-    double s1, e1, s2, e2, s3, e3, s4, e4;
-    two_sum(fn.x, -fk.x, s1, e1);
-    two_sum(s1, -fm.x, s2, e2);
-    const double p1 = k * cp.logp, f1 = fma(k, cp.logp, -p1);       // exact products: p + f = k * logp
-    const double p2 = m * cp.log1mp, f2 = fma(m, cp.log1mp, -p2);
+    double s3, e3, s4, e4;
+    const double p1 = k * logp, f1 = fma(k, logp, -p1);               // exact products: p + f = k * logp
+    const double p2 = m * log1mp, f2 = fma(m, log1mp, -p2);
     two_sum(p1, p2, s3, e3);
     two_sum(s2, s3, s4, e4);
-    double lo = (fn.y - fk.y) - fm.y;
-    lo = lo + ((e1 + e2) + (e3 + e4));
+    double lo = lt + (e3 + e4);
     lo = lo + (f1 + f2);
-    lo = lo + (k * cp.logp_lo + m * cp.log1mp_lo);
+    lo = lo + (k * logp_lo + m * log1mp_lo);
     return LogW{s4, lo};
 }
 
-// sum of the magnitudes of binom_logpmf_hi's terms (+1): its result is within ~8 ulps of this (8 roundings, each
-// at most half an ulp of a partial sum bounded by it)
-__device__ __forceinline__ double logw_scale(double k, double n, const ChainParam& cp, const double2* lf, int lf_max) {
-    const int ni = min(max((int)n, 0), lf_max);
-    return (2.0 * fabs(lf[ni].x) + fabs(k * cp.logp)) + (fabs((n - k) * cp.log1mp) + 1.0);
+// the compensated log pmf with scipy's special cases (lo = 0 there)
+__device__ __forceinline__ LogW binom_logpmf(double k, double n, const ChainParam& cp, const double* lf, int lf_max) {
+    double s2, e12;
+    LfIdx ix;
+    const double h = binom_logpmf_plain(k, n, cp, lf, lf_max, s2, e12, ix);
+    const double p = cp.probs;
+    if (!(h > -__builtin_inf()) || p == 0.0 || p == 1.0) return LogW{h, 0.0};   // NaN, pmf 0, or pmf 0 / 1 cases
+    return binom_logpmf_core(k, n, s2, e12, ix, lf, lf_max, cp.logp, cp.log1mp, cp.logp_lo, cp.log1mp_lo);
 }
 
 // a < b for compensated logs of nearby size (hi - hi is exact within a factor 2, Sterbenz); -inf and NaN by hi
@@ -933,14 +954,42 @@ __device__ __forceinline__ double observed(const double* x, int i) {
     }
 }
 
+// The binomial weight when two columns' plain logs tie within their error: every column compensated, the smallest
+// by the compensated logs.  Out of line (rare, ~1e-6 of particle-steps at config 2): the state comes back from its
+// just-written row (`row`, int32 [C]) and the chain's parameters from global memory, so the call passes no arrays
+// and the step kernel keeps its registers for the event loop.
+template <int MODEL, int G>
+__device__ __attribute__((noinline)) double binom_weight_tied(const int32_t* row, const double* yrow,
+                                                              const ChainParam* cpp, const double* lf, int lf_max) {
+    constexpr int K = Shape<MODEL, G>::K, C = Shape<MODEL, G>::C;
+    const ChainParam& cp = *cpp;
+    double x[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = (double)row[c];
+    LogW L = binom_logpmf(yrow[0], observed<MODEL, G>(x, 0), cp, lf, lf_max);
+#pragma unroll
+    for (int i = 1; i < K; ++i) {
+        const LogW li = binom_logpmf(yrow[i], observed<MODEL, G>(x, i), cp, lf, lf_max);
+        if (logw_less(li, L)) L = li;
+    }
+    const double e = exp(L.hi);
+    return fma(e, L.lo, e);
+}
+
 // min over the K observed columns (np.min propagates NaN), pmcmc.py:178-181.  Binomial: exp is monotone, so the
-// minimum is taken on the logs and exponentiated once.  The columns are ranked on their plain-double logs; only
-// the smallest is evaluated compensated -- unless another column lies within the plain logs' error of it (a
-// near tie, wave-uniform branch: rare), when every column is, and the compensated logs decide.  The plain log's
-// error is a few ulps of log n! (<= 2^-48 |lf_hi[n]| with margin), so outside a near tie the ranking is exact.
+// minimum is taken on the logs and exponentiated once.  The columns are ranked on their plain-double logs (one
+// round of table loads, which also yields the table parts of the compensated value); only the smallest is then
+// compensated -- unless another column lies within the plain logs' error of it (a near tie: binom_weight_tied,
+// every column compensated).  The plain log's error is a few ulps of the sum of its terms' magnitudes, which the
+// host bounds per chain (cp.tie_tol, 8x that bound), so outside a near tie the ranking is exact.
+// cp: the chain's parameters as the kernel holds them (probs, log p, log1p(-p)); the lo parts and tie_tol are read
+// from cpp here, behind a compiler barrier (their loads overlap the table loads): carried from the kernel's start,
+// live across the event loop, they cost the step kernels ~40 SGPR spills.  row: this particle's state as stored in
+// the history (int32 [C]), read only on the tie path.
 template <int MODEL, int G, int OBS>
 __device__ __forceinline__ double particle_weight(const double* x, const double* yrow, const ChainParam& cp,
-                                                  const double2* lf, int lf_max) {
+                                                  const ChainParam* cpp, const double* lf, int lf_max,
+                                                  const int32_t* row) {
     constexpr int K = Shape<MODEL, G>::K;
     if constexpr (OBS == kNormal) {
         double w = 0.0;
@@ -952,45 +1001,35 @@ __device__ __forceinline__ double particle_weight(const double* x, const double*
         }
         return w;
     } else {
-        double lh[K], xo[K];
-        double m = 0.0;
-        int am = 0;
+        asm volatile("" ::: "memory");
+        const double logp_lo = cpp->logp_lo, log1mp_lo = cpp->log1mp_lo, tie_tol = cpp->tie_tol;
+        double lh[K];
+        double m = 0.0, ys = 0.0, xs = 0.0, s2m = 0.0, e12m = 0.0;   // the running minimum and its operands
+        LfIdx ixm{0, 0, 0};
 #pragma unroll
         for (int i = 0; i < K; ++i) {
-            xo[i] = observed<MODEL, G>(x, i);
-            lh[i] = binom_logpmf_hi(yrow[i], xo[i], cp, lf, lf_max);
-            if (i == 0 || isnan(lh[i])) { m = lh[i]; am = i; }
-            else if (!isnan(m) && lh[i] < m) { m = lh[i]; am = i; }
+            const double xo = observed<MODEL, G>(x, i);
+            double s2, e12;
+            LfIdx ix;
+            lh[i] = binom_logpmf_plain(yrow[i], xo, cp, lf, lf_max, s2, e12, ix);
+            const bool take = (i == 0 || isnan(lh[i])) || (!isnan(m) && lh[i] < m);
+            m = take ? lh[i] : m;
+            ys = take ? yrow[i] : ys;
+            xs = take ? xo : xs;
+            s2m = take ? s2 : s2m;
+            e12m = take ? e12 : e12m;
+            ixm.n = take ? ix.n : ixm.n;
+            ixm.k = take ? ix.k : ixm.k;
+            ixm.m = take ? ix.m : ixm.m;
         }
-        if (isnan(m)) return m;
-        // the minimum's operands, selected without indexing (registers)
-        double ys = yrow[0], xs = xo[0];
+        if (isnan(m)) return m;                                        // np.min propagates NaN
+        if (!(m > -__builtin_inf())) return 0.0;                       // a column outside its support: pmf 0
+        if (cp.probs == 0.0 || cp.probs == 1.0) return 1.0;            // m finite: every column's pmf is 1
+        int below = 0;                                                 // columns within tie_tol of the minimum
 #pragma unroll
-        for (int i = 1; i < K; ++i) {
-            ys = (am == i) ? yrow[i] : ys;
-            xs = (am == i) ? xo[i] : xs;
-        }
-        bool tie = false;
-        if (m > -__builtin_inf()) {
-            const double sm = logw_scale(ys, xs, cp, lf, lf_max);
-#pragma unroll
-            for (int i = 0; i < K; ++i) {
-                if (i == am || (yrow[i] == ys && xo[i] == xs)) continue;     // identical operands: identical value
-                const double tol = (sm + logw_scale(yrow[i], xo[i], cp, lf, lf_max)) * 0x1.0p-46;
-                tie = tie || (lh[i] - m <= tol);
-            }
-        }
-        LogW L;
-        if (tie) {
-            L = binom_logpmf(yrow[0], xo[0], cp, lf, lf_max);
-#pragma unroll
-            for (int i = 1; i < K; ++i) {
-                const LogW li = binom_logpmf(yrow[i], xo[i], cp, lf, lf_max);
-                if (logw_less(li, L)) L = li;
-            }
-        } else {
-            L = binom_logpmf(ys, xs, cp, lf, lf_max);
-        }
+        for (int i = 0; i < K; ++i) below += (lh[i] - m <= tie_tol) ? 1 : 0;
+        if (below > 1) return binom_weight_tied<MODEL, G>(row, yrow, cpp, lf, lf_max);
+        const LogW L = binom_logpmf_core(ys, xs, s2m, e12m, ixm, lf, lf_max, cp.logp, cp.log1mp, logp_lo, log1mp_lo);
         const double e = exp(L.hi);
         return fma(e, L.lo, e);                                        // exp(hi + lo) = exp(hi) (1 + lo)
     }
@@ -1036,7 +1075,9 @@ __device__ __forceinline__ double cert_halfwidth(int i, double v, double cert_k)
 // The reference's own CDF is numpy's over scipy's weights, which differ from the device's by at most E relative
 // each (E: scipy's error envelope plus the device's).  Then |cdf_ref_i - cdf_i| <= 2E v (1 - v)
 // (1 + tiny), and ref_k = 2E (1 + 2^-10).  A draw whose U lies within delta_i + that of a boundary of its answer
-// may differ from the reference's: counted (resample_ref_ambiguous), never changed.
+// may differ from the reference's: counted (resample_ref_ambiguous), never changed.  Every uncertified draw (U
+// within delta of a boundary) is counted too, without a finer test against the exact CDF: carrying that test
+// into resample_exact_wave cost the step kernels 16 SGPR spills (a v_readlane per use on every step).
 __device__ __forceinline__ double ref_halfwidth(double v, double ref_k) {
     return ref_k * (v * (1.0 - v));
 }
@@ -1101,8 +1142,9 @@ __device__ __forceinline__ int resample_search(double U, const double* bpex, con
                               : (b > 0 ? (bpex[b - 1] + bsum[b - 1]) / total : -1.0);
     certified = (va - cert_halfwidth(a, va, cert_k) > U) &&
                 (a == 0 || vp + cert_halfwidth(a - 1, vp, cert_k) < U) && a < N;
-    ambiguous = !((va - (cert_halfwidth(a, va, cert_k) + ref_halfwidth(va, ref_k)) > U) &&
-                  (a == 0 || vp + (cert_halfwidth(a - 1, vp, cert_k) + ref_halfwidth(vp, ref_k)) < U));
+    if (ref_k > 0.0)                          // counting on (ref_k = 0 otherwise: the test costs ~10 VALU per draw)
+        ambiguous = !((va - (cert_halfwidth(a, va, cert_k) + ref_halfwidth(va, ref_k)) > U) &&
+                      (a == 0 || vp + (cert_halfwidth(a - 1, vp, cert_k) + ref_halfwidth(vp, ref_k)) < U));
     return a;
 }
 
@@ -1152,8 +1194,9 @@ __device__ __forceinline__ int resample_search_seg(double U, const double* seg_s
     const double vp = (l > 0) ? (base + L[l - 1]) / total : (b > 0 ? pb / total : -1.0);
     certified = (va - cert_halfwidth(a, va, cert_k) > U) &&
                 (a == 0 || vp + cert_halfwidth(a - 1, vp, cert_k) < U) && a < N;
-    ambiguous = !((va - (cert_halfwidth(a, va, cert_k) + ref_halfwidth(va, ref_k)) > U) &&
-                  (a == 0 || vp + (cert_halfwidth(a - 1, vp, cert_k) + ref_halfwidth(vp, ref_k)) < U));
+    if (ref_k > 0.0)                          // counting on (ref_k = 0 otherwise: the test costs ~10 VALU per draw)
+        ambiguous = !((va - (cert_halfwidth(a, va, cert_k) + ref_halfwidth(va, ref_k)) > U) &&
+                      (a == 0 || vp + (cert_halfwidth(a - 1, vp, cert_k) + ref_halfwidth(vp, ref_k)) < U));
     return a;
 }
 
@@ -1206,8 +1249,7 @@ struct ChunkStream {
     }
 };
 
-__device__ __forceinline__ int resample_exact_wave(bool need, double U, const double* __restrict__ w, int N,
-                                                   double ref_k, bool& ambiguous) {
+__device__ __forceinline__ int resample_exact_wave(bool need, double U, const double* __restrict__ w, int N) {
     ChunkStream cs;
     // pass 1: S
     double S = 0.0;
@@ -1243,25 +1285,16 @@ __device__ __forceinline__ int resample_exact_wave(bool need, double U, const do
     bool waiting = need;
     ExactTarget tg = exact_next_target(waiting, U);
     c = 0.0;
-    double cprev = 0.0;
     cs.start(w, N);
 #pragma unroll 1
     for (int cb = 0; cb < N && !tg.done; cb += 64) {
         const double q = cs.next(cb) / S;
         const int n = min(64, N - cb);
         for (int l = 0; l < n; ++l) {
-            cprev = c;
             c = c + readlane_f64(q, l);
             const double r = c * rl;
             while (!tg.done && r > tg.lo && (r > tg.hi || c / last > tg.U)) {   // cdf_i > U*: lanes at U* done
-                if (waiting && U == tg.U) {
-                    ans = cb + l;
-                    waiting = false;
-                    // cdf_{i-1} <= U < cdf_i exactly; the reference's boundaries are within ref_halfwidth of them
-                    const double ci = c / last, cp = cprev / last;
-                    ambiguous = (ci - U <= ref_halfwidth(ci, ref_k)) ||
-                                (cb + l > 0 && U - cp <= ref_halfwidth(cp, ref_k));
-                }
+                if (waiting && U == tg.U) { ans = cb + l; waiting = false; }
                 tg = exact_next_target(waiting, U);
             }
             if (tg.done) break;

@@ -308,14 +308,14 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
                     anc = resample_search_seg<true>(U, seg_start, seg_end, a.nseg, a.seg, a.bsum + bprev, a.B, total,
                                               a.wloc + wprev, 64, a.N, a.cert_k, certified, a.ref_k, ambiguous);
             }
+            if (ambiguous) atomicAdd(counter_slot(a.counters) + 6, 1ull);
             if (__any(!certified)) {
-                const int e = resample_exact_wave(!certified, U, a.wraw + wprev, a.N, a.ref_k, ambiguous);
+                const int e = resample_exact_wave(!certified, U, a.wraw + wprev, a.N);
                 if (!certified) {
                     anc = e;
                     atomicAdd(counter_slot(a.counters) + 1, 1ull);
                 }
             }
-            if (ambiguous) atomicAdd(counter_slot(a.counters) + 6, 1ull);
             if (j < a.N) {                               // :193-199
                 anc = checked_index(anc, a.N);
                 a.ancestry[(size_t)chain * a.anc_stride + (size_t)p * a.N + j] = anc;
@@ -366,7 +366,8 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
             int32_t* hc = a.hidden + (size_t)chain * a.hist_stride + ((size_t)p * a.N + j) * C;
 #pragma unroll
             for (int c = 0; c < C; ++c) hc[c] = (int32_t)xs[c];                       // :222-231
-            if (p + 1 < a.T) w = particle_weight<MODEL, G, OBS>(xs, a.Y + (size_t)p * Sh::K, cp, a.lf, a.lf_max);
+            if (p + 1 < a.T)
+                w = particle_weight<MODEL, G, OBS>(xs, a.Y + (size_t)p * Sh::K, cp, a.cp + chain, a.lf, a.lf_max, hc);
         }
         if (p + 1 < a.T) {
             const double loc = block_inclusive_scan<64>(w, red);

@@ -35,7 +35,7 @@ __device__ __forceinline__ unsigned long long* counter_slot(unsigned long long* 
 //   wloc     f64   [2][max_chains][B*WG]          in-block inclusive prefix of wraw
 //   bsum     f64   [2][max_chains][B]             block totals
 //   log_zeta f64   [max_chains][T]
-//   Y        f64   [T][K];  lf f64x2 [lf_max+1] = log n! as hi + lo (binary128 on the host, logfact.cpp)
+//   Y        f64   [T][K];  lf f64 [2][lf_max+1] = log n! as hi, then lo (binary128 on the host, logfact.cpp)
 struct StepArgs {
     int N, T, B, wg, max_chains, resample_mode, count_events, lf_max;
     int chain0;                   // first chain of this launch (chain groups run on separate streams)
@@ -47,7 +47,7 @@ struct StepArgs {
     double cert_k;                // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp)
     double ref_k;                 // 2E (1 + 2^-10): reference-ambiguity bracket (ref_halfwidth)
     const double* Y;
-    const double2* lf;            // (hi, lo) of log n!, n = 0..lf_max (binom_logpmf)
+    const double* lf;             // log n!, n = 0..lf_max: hi parts, then lo parts (binom_logpmf_plain)
     const LogTab* logtab;         // glibc log table [kLogTabEntries] (context-resident)
     const ChainParam* cp;
     int32_t* hidden;

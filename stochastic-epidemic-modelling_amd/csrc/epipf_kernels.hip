@@ -60,7 +60,9 @@ __global__ __launch_bounds__(WG) void pf_init_kernel(StepArgs a) {
     if (bp.b == 0 && threadIdx.x == 0) a.log_zeta[(size_t)chain * a.T] = 0.0;
     if (a.T > 1) {
         double w = 0.0;
-        if (j < a.N) w = particle_weight<MODEL, G, OBS>(x, a.Y, cp, a.lf, a.lf_max);
+        if (j < a.N)
+            w = particle_weight<MODEL, G, OBS>(x, a.Y, cp, a.cp + chain, a.lf, a.lf_max,
+                                               a.hidden + (size_t)chain * a.hist_stride + (size_t)j * C);
         const size_t wbase = (size_t)chain * a.wstride;            // buffer 0
         const double loc = block_inclusive_scan<WG>(w, smem);
         a.wraw[wbase + j] = w;
@@ -127,14 +129,16 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
             anc = resample_search_seg(U, seg_start, seg_end, a.nseg, a.seg, a.bsum + bprev, a.B, total,
                                       a.wloc + wprev, WG, a.N, a.cert_k, certified, a.ref_k, ambiguous);
     }
+    // reference-ambiguous draws (rare: ~1e-8 of draws at config 2; every uncertified one included), counted with
+    // the other device counters (EPIPF_PROFILE_COUNTERS: bench.py's untimed counters iteration, the parity tests)
+    if (ambiguous) atomicAdd(counter_slot(a.counters) + 6, 1ull);
     if (__any(!certified)) {   // wave-uniform: the whole wave resolves its uncertified draws exactly
-        const int e = resample_exact_wave(!certified, U, a.wraw + wprev, a.N, a.ref_k, ambiguous);
+        const int e = resample_exact_wave(!certified, U, a.wraw + wprev, a.N);
         if (!certified) {
             anc = e;
             atomicAdd(counter_slot(a.counters) + 1, 1ull);
         }
     }
-    if (ambiguous) atomicAdd(counter_slot(a.counters) + 6, 1ull);   // rare (~1e-8 of draws at config 2)
     // (f) gather the parent state, (g) propagate over [0, 1], :195-220: the certified f32 loop, then the exact path
     // for the lanes it hands back.  The exact path's log table is copied to LDS only by waves that need it (~1% at
     // config 2): one wave per block, so the wave-uniform test is block-uniform and the barriers are legal.
@@ -190,7 +194,7 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
 #pragma unroll
         for (int c = 0; c < C; ++c) hc[c] = (int32_t)x[c];                        // :222-231
         // (a) weights of the new state against Y[p], used by step p+1, :178-181
-        if (p + 1 < a.T) w = particle_weight<MODEL, G, OBS>(x, a.Y + (size_t)p * Sh::K, cp, a.lf, a.lf_max);
+        if (p + 1 < a.T) w = particle_weight<MODEL, G, OBS>(x, a.Y + (size_t)p * Sh::K, cp, a.cp + chain, a.lf, a.lf_max, hc);
     }
     if (a.count_events) {  // accepted events; lane-iterations; wave-iterations x 64 (lane utilisation)
         unsigned long long e = (unsigned long long)nev, li = (unsigned long long)iters;
@@ -329,7 +333,7 @@ __global__ __launch_bounds__(WG) void resample_search_kernel(ResampleArgs a) {
     int anc = 0;
     if (j < a.N) anc = resample_search<WG>(U, bpex, bsum, a.B, total, a.wloc, a.N, a.cert_k, certified, 0.0, ambiguous);
     if (__any(!certified)) {
-        const int e = resample_exact_wave(!certified, U, a.wraw, a.N, 0.0, ambiguous);
+        const int e = resample_exact_wave(!certified, U, a.wraw, a.N);
         if (!certified) {
             anc = e;
             atomicAdd(a.fallbacks, 1ull);

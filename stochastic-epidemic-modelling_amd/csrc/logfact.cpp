@@ -21,25 +21,27 @@ inline void split(__float128 q, double* hi, double* lo) {
     *lo = std::isfinite(h) ? (double)(q - (__float128)h) : 0.0;
 }
 
-void fill(int from, int to, double* out) {
-    for (int n = from; n < to; ++n) split(lgammaq((__float128)n + 1), &out[2 * (size_t)n], &out[2 * (size_t)n + 1]);
+void fill(int from, int to, double* hi, double* lo) {
+    for (int n = from; n < to; ++n) split(lgammaq((__float128)n + 1), &hi[n], &lo[n]);
 }
 
 }  // namespace
 
 namespace epipf {
 
-// out[2n], out[2n+1] = hi, lo of log(n!) for n = 0..n_max (lgammaq: ~2 us per entry, threaded above 64k entries)
+// out[n] = hi and out[n_max + 1 + n] = lo of log(n!) for n = 0..n_max (lgammaq: ~2 us per entry, threaded above
+// 64k entries)
 void logfact_table(int n_max, double* out) {
     const int n = n_max + 1;
+    double* lo = out + n;
     const int threads = n > 65536 ? (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1;
     if (threads == 1) {
-        fill(0, n, out);
+        fill(0, n, out, lo);
         return;
     }
     std::vector<std::thread> pool;
     for (int t = 0; t < threads; ++t)
-        pool.emplace_back(fill, (int)((long)n * t / threads), (int)((long)n * (t + 1) / threads), out);
+        pool.emplace_back(fill, (int)((long)n * t / threads), (int)((long)n * (t + 1) / threads), out, lo);
     for (auto& th : pool) th.join();
 }
 

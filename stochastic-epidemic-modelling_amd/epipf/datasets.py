@@ -4,9 +4,12 @@
   *_simulate_discrete                            pmcmc.py:54-113  (odeint, then the last sample of each ceil-day)
   thin_binomial                                  tests/test_pmcmc_p.py:21-29, tests/test_simulations_subgroups.py:57-64
   noise_normal                                   tests/test_pmcmc_noisy.py:21-29 (Gaussian noise, cast to int)
-Returned arrays drop the reference's pandas DataFrame wrapper: discrete series are [days, 1 + C] with the
-time column first (the DataFrame's column order for SIR/SEIR).  `benchmark_dataset(cfg)` builds the
-BASELINE.json configurations.
+The reference-named `*_simulate_discrete` return the reference's pandas DataFrame (same columns, same dtypes: an
+integer `time` day column, then `susceptible`/`exposed`/`infected`/`removed`, or `susceptible0, infected0,
+removed0, ...` then `time` for the subgroup model), so reference scripts reading `data.time` / `data.susceptible0`
+run unchanged; without pandas they return the same table as an ndarray.  `*_discrete_array` are the bare arrays
+([days, 1 + C], sample times not rounded to days) the rest of the package uses.  `benchmark_dataset(cfg)` builds
+the BASELINE.json configurations.
 
 Integrator ("regenerate fixtures without scipy"): the reference calls scipy's `odeint`
 (ODEPACK LSODA).  `integrator="odeint"` uses it (bit-identical to the reference); `integrator="dopri5"` is a
@@ -113,24 +116,63 @@ def _last_sample_per_day(t, solution):
     return rows
 
 
-def sir_simulate_discrete(y0, t, beta, gamma, integrator=None):
+def sir_discrete_array(y0, t, beta, gamma, integrator=None):
+    """[days, 4]: sample time, S, I, R at the last ODE sample of each ceil-day (pmcmc.py:54-73 without pandas)."""
     sol = _integrate(differential_sir, y0, t, (beta, gamma), integrator)
     rows = _last_sample_per_day(t, sol)
     return np.column_stack([np.asarray(t)[rows], sol[rows]])
 
 
-def seir_simulate_discrete(y0, t, beta, alpha, gamma, integrator=None):
+def seir_discrete_array(y0, t, beta, alpha, gamma, integrator=None):
+    """[days, 5]: sample time, S, E, I, R (pmcmc.py:76-96 without pandas)."""
     sol = _integrate(differential_seir, y0, t, (beta, alpha, gamma), integrator)
     rows = _last_sample_per_day(t, sol)
     return np.column_stack([np.asarray(t)[rows], sol[rows]])
 
 
-def sir_subgroups_simulate_discrete(y0, t, beta, gamma, integrator=None):
-    """Columns: S0, I0, R0, S1, ... then time LAST (pmcmc.py:99-113 DataFrame order)."""
+def sir_subgroups_discrete_array(y0, t, beta, gamma, integrator=None):
+    """[days, 3G + 1]: S0, I0, R0, S1, ... then the sample time LAST (pmcmc.py:99-113 column order)."""
     y0 = [i for item in np.asarray(y0).tolist() for i in item]
     sol = _integrate(differential_sir_subgroups, y0, t, (np.asarray(beta).tolist(), gamma), integrator)
     rows = _last_sample_per_day(t, sol)
     return np.column_stack([sol[rows], np.asarray(t)[rows]])
+
+
+def _frame(columns, arr, time_col):
+    """The reference's returned table: the day column is np.ceil(time).astype(int) (pmcmc.py:66, :89, :106), the
+    rest float64, index 0..days-1.  An ndarray with the same values when pandas is not importable."""
+    days = np.ceil(arr[:, time_col]).astype(int)
+    try:
+        import pandas as pd
+    except ImportError:
+        out = arr.copy()
+        out[:, time_col] = days
+        return out
+    data = {c: (days if i == time_col else arr[:, i]) for i, c in enumerate(columns)}
+    return pd.DataFrame(data, columns=columns)
+
+
+def sir_simulate_discrete(y0, t, beta, gamma, integrator=None):
+    """pmcmc.py:54-73: DataFrame (time, susceptible, infected, removed), one row per day."""
+    return _frame(["time", "susceptible", "infected", "removed"],
+                  sir_discrete_array(y0, t, beta, gamma, integrator), 0)
+
+
+def seir_simulate_discrete(y0, t, beta, alpha, gamma, integrator=None):
+    """pmcmc.py:76-96: DataFrame (time, susceptible, exposed, infected, removed), one row per day."""
+    return _frame(["time", "susceptible", "exposed", "infected", "removed"],
+                  seir_discrete_array(y0, t, beta, alpha, gamma, integrator), 0)
+
+
+def sir_subgroups_simulate_discrete(y0, t, beta, gamma, integrator=None):
+    """pmcmc.py:99-113: DataFrame (susceptible0, infected0, removed0, susceptible1, ..., time), one row per day."""
+    arr = sir_subgroups_discrete_array(y0, t, beta, gamma, integrator)
+    G = (arr.shape[1] - 1) // 3
+    cols = [f"{c}{g}" for g in range(G) for c in ("susceptible", "infected", "removed")] + ["time"]
+    return _frame(cols, arr, arr.shape[1] - 1)
+
+
+differential_sir_subroups = differential_sir_subgroups   # the reference's spelling (pmcmc.py:37)
 
 
 def thin_binomial(values, prob, rs):
@@ -144,27 +186,27 @@ def noise_normal(values, ratio, rs):
 def benchmark_dataset(cfg, integrator=None):
     """Observation matrices for the BASELINE.json configs.  Returns (Y, meta)."""
     if cfg == 1:
-        ode = sir_simulate_discrete((180, 20, 0), np.linspace(0, 49, num=500), 2, 1,
+        ode = sir_discrete_array((180, 20, 0), np.linspace(0, 49, num=500), 2, 1,
                                     integrator=integrator)[:, 1:]
         return thin_binomial(ode, 0.1, np.random.RandomState(2)), dict(
             model="sir", n_population=200, mu=20, theta=(2.0, 1.0), probs=0.1, N=100,
             describe="ODE SIR y0=(180,20,0), beta=2, gamma=1, 50 daily rows, binomial thinning p=.1, RandomState(2)")
     if cfg == 2:
-        ode = sir_simulate_discrete((9980, 20, 0), np.linspace(0, 199, num=2000), 0.25, 0.1,
+        ode = sir_discrete_array((9980, 20, 0), np.linspace(0, 199, num=2000), 0.25, 0.1,
                                     integrator=integrator)[:, 1:]
         return thin_binomial(ode, 0.1, np.random.RandomState(1)), dict(
             model="sir", n_population=10000, mu=20, theta=(0.25, 0.1), probs=0.1, N=10000,
             describe="ODE SIR y0=(9980,20,0), beta=.25, gamma=.1, 200 daily rows, binomial thinning p=.1, "
                      "RandomState(1)")
     if cfg == 3:
-        ode = seir_simulate_discrete((9980, 0, 20, 0), np.linspace(0, 199, num=2000), 0.5, 0.2, 0.1,
+        ode = seir_discrete_array((9980, 0, 20, 0), np.linspace(0, 199, num=2000), 0.5, 0.2, 0.1,
                                      integrator=integrator)[:, 1:]
         return noise_normal(ode, 0.1, np.random.RandomState(3)), dict(
             model="seir", n_population=10000, mu=20, theta=(0.5, 0.2, 0.1), probs=0.1, observations=True, N=10000,
             describe="ODE SEIR y0=(9980,0,20,0), beta=.5, alpha=.2, gamma=.1, 200 daily rows, Gaussian noise "
                      "N(x, .1x) cast to int, RandomState(3); normal observation model")
     if cfg == 4:
-        ode = sir_simulate_discrete((4800, 20, 0), np.linspace(0, 14, num=200), 2, 1,
+        ode = sir_discrete_array((4800, 20, 0), np.linspace(0, 14, num=200), 2, 1,
                                     integrator=integrator)[:, 1:]
         return thin_binomial(ode, 0.1, np.random.RandomState(11)), dict(
             model="sir", n_population=4820, mu=20, theta=(2.0, 1.0), probs=0.1, N=50000,

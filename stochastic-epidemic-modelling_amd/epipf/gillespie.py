@@ -40,8 +40,9 @@ def simulate_path_batch(type_model, states, theta, max_time=1.0, *, key=None, fi
 
 def _path_dict(names, x0, times, states, n, time_first):
     """The reference's conditions dict: the initial value then one entry per event (gillespie_algo.py:68-70);
-    counts keep the type of the caller's population entries, as the reference's `value + stoichiometry` does."""
-    conv = [type(v.item() if isinstance(v, np.generic) else v) for v in x0]
+    counts keep the type of the caller's population entries, as the reference's `value + stoichiometry` does
+    (np.int64 entries give np.int64 counts, Python ints give ints, floats give floats)."""
+    conv = [type(v) for v in x0]
     cols = {}
     for c, name in enumerate(names):
         cols[name] = [x0[c]] + [conv[c](v) for v in states[:n, c].tolist()]
@@ -50,7 +51,8 @@ def _path_dict(names, x0, times, states, n, time_first):
 
 
 def _one_path(model, names, population, theta, max_time, time_first, key, filter_index, step):
-    flat = np.asarray(population, dtype=object).reshape(-1).tolist()
+    pop = population if isinstance(population, np.ndarray) else np.asarray(population, dtype=object)
+    flat = list(pop.reshape(-1))          # the caller's elements: numpy scalars stay numpy scalars
     t, x, n, _ = simulate_path_batch(model, np.asarray(flat, dtype=float).reshape(1, -1), theta, max_time, key=key,
                                      filter_index=filter_index, step=step)
     return _path_dict(names, flat, t[0], x[0], int(n[0]), time_first)

@@ -198,6 +198,10 @@ class ChainSampler:
         P = np.asarray(parameters, dtype=np.float64)
         d = self.d = P.shape[-1]
         # per-chain starting points (a [chains, d] array, e.g. warm starts, chains_io.warm_start) or one for all
+        if P.ndim == 2 and P.shape[0] != nc:
+            raise ValueError(f"parameters has {P.shape[0]} per-chain rows for {nc} chains")
+        if P.ndim not in (1, 2):
+            raise ValueError("parameters must be [d] or [chains, d]")
         self.params = [(P[c] if P.ndim == 2 else P).tolist() for c in range(nc)]
         self.parameters = self.params[0] if nc else P.tolist()
         self.probs = probs
@@ -230,6 +234,10 @@ class ChainSampler:
         self._tr = np.zeros((nc, self.iters, T, Cc))
         self.trajs = self._tr.transpose(0, 2, 1, 3)
         S = None if sigma is None else np.asarray(sigma, dtype=np.float64)
+        if S is not None and S.ndim == 3 and S.shape[0] != nc:
+            raise ValueError(f"sigma has {S.shape[0]} per-chain matrices for {nc} chains")
+        if S is not None and (S.ndim not in (2, 3) or S.shape[-2:] != (d, d)):
+            raise ValueError(f"sigma must be [{d}, {d}] or [chains, {d}, {d}]")
         self.std = [np.eye(d) if S is None else (S[c] if S.ndim == 3 else S).copy() for c in range(nc)]
         self._fac = [None] * nc                                  # multivariate_normal factor of h * std[c]
         self.fnext = [int(filter_index_start)] * nc

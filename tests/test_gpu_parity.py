@@ -593,6 +593,7 @@ def test_full_size_baseline_configs_vs_oracle(cfg, chains, lanes, streams, check
     eng.set_observations(Y)
     eng.set_population(meta["n_population"], meta["mu"])
     eng.set_lanes(lanes)
+    eng.set_profiling(2)                   # device counters on: reference-ambiguous draws are counted
     if streams:
         eng.set_streams(streams)
     obs = bool(meta.get("observations", False))

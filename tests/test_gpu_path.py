@@ -112,8 +112,9 @@ def test_dropin_full_path_dicts(path_golden):
         assert cond["time"][0] == 0.0 and cond["time"][1:] == tj.tolist()
         for c, col in enumerate(cols):
             assert cond[col] == [x0[c]] + xj[:, c].tolist()
-            want = int if name.startswith("path_sub") else float
-            assert all(type(v) is want for v in cond[col][1:])
+            # the reference's counts are population[...] + stoichiometry: np.int64 for an int64 array, float for floats
+            want = np.int64 if name.startswith("path_sub") else float
+            assert all(type(v) is want for v in cond[col]), (col, {type(v) for v in cond[col]})
         last = gl.sir_simulate([float(v) for v in x0], np.array(rec["theta"]), float(rec["max_time"]), True, **kw) \
             if name.startswith("path_sir") else None
         if last is not None:
