@@ -1,0 +1,94 @@
+"""Ancestors against the reference itself at bench scale.
+
+Runs the filters of the bench layout on the GPU (BASELINE config 2 by default: 256 chains x N = 10^4 x T = 200, the
+bench's keys, thetas around its start; launches of --slice chains), with the device counters on, then replays every step of every chain the reference's way
+on the host -- scipy.stats.binom.pmf / norm.pdf weights of the device's own states, numpy legacy choice on the keyed
+uniforms (tests/reference_replay.py) -- and counts ancestors that differ.  Also reports the device's
+reference-ambiguity count (draws whose uniform lies within scipy's error envelope of a CDF boundary) and its
+uncertified draws for the same launch.  Writes profiles/r3_ref_replay_cfg<config>.json.
+
+    python scripts/r3_ref_replay.py [--config 2] [--chains 256] [--workers 12]"""
+import argparse
+import json
+import os
+import sys
+import time
+from concurrent.futures import ProcessPoolExecutor
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "stochastic-epidemic-modelling_amd"), os.path.join(REPO, "oracle"),
+                os.path.join(REPO, "tests")]
+
+
+def _noop(_):
+    import reference_replay  # noqa: F401  (scipy imported once per worker)
+    return 0
+
+
+def _replay(job):
+    import reference_replay
+    Y, hid, anc, model, obs, probs, key, f = job
+    return reference_replay.replay(Y, hid, anc, model, obs, probs, key, f)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--chains", type=int, default=256)
+    ap.add_argument("--slice", type=int, default=16, help="chains copied to the host at a time")
+    ap.add_argument("--workers", type=int, default=12)
+    ap.add_argument("--seed", type=int, default=2024)
+    args = ap.parse_args()
+    # the replay workers are forked (and started) before anything touches the GPU
+    pool = ProcessPoolExecutor(args.workers)
+    list(pool.map(_noop, range(args.workers)))
+    from epipf import _lib, datasets
+    from epipf.engine import Engine
+    from epipf.pmcmc import chain_key
+    Y, meta = datasets.benchmark_dataset(args.config)
+    G = len(np.atleast_1d(meta["n_population"]))
+    th = np.asarray(meta["theta"], dtype=np.float64)
+    C, N, T = args.chains, meta["N"], Y.shape[0]
+    obs = bool(meta.get("observations", False))
+    eng = Engine(meta["model"], G, N, T, args.slice)
+    eng.set_observations(Y)
+    eng.set_population(meta["n_population"], meta["mu"])
+    eng.set_lanes(1)                                      # the bench's kernel (one lane per particle)
+    eng.set_profiling(_lib.PROFILE_COUNTERS)
+    keys = [chain_key(args.seed, g) for g in range(C)]
+    rs = np.random.RandomState(args.seed)
+    thetas = np.abs(th[None] * (1.0 + 0.05 * rs.standard_normal((C, th.size))))   # around the bench's start
+    t0 = time.time()
+    draws = bad = n_ok = 0
+    mname = meta["model"]
+    # chains in launches of `slice` (a chain's results do not depend on its batch: test_batched_chains_equal_single_runs)
+    with pool:
+        for lo in range(0, C, args.slice):
+            n = min(args.slice, C - lo)
+            lz, st = eng.run(thetas[lo:lo + n], [meta["probs"]] * n, keys[lo:lo + n], [1] * n, observations=obs)
+            hid, anc = eng.history(n)
+            jobs = [(Y, hid[c], anc[c], mname, obs, meta["probs"], keys[lo + c], 1) for c in range(n) if st[c] == 0]
+            n_ok += len(jobs)
+            del hid, anc
+            for d, b in pool.map(_replay, jobs):
+                draws += d
+                bad += b
+            print(f"chains {lo + n}/{C}: {draws} draws replayed, {bad} differ", flush=True)
+    stats = eng.stats()
+    eng.close()
+    out = {"config": args.config, "chains": C, "chains_ok": n_ok, "N": N, "T": T, "draws_replayed": draws,
+           "ancestors_differing_from_reference": bad, "device_resample_ref_ambiguous": stats["resample_ref_ambiguous"],
+           "device_resample_draws": C * N * (T - 1), "device_uncertified_draws": stats["resample_fallbacks"],
+           "library_build_id": _lib.build_id(), "seconds": time.time() - t0,
+           "method": "device states -> scipy.stats weights (pmcmc.py:177-181) -> numpy legacy choice on the keyed "
+                     "uniforms (pmcmc.py:185-190), tests/reference_replay.py"}
+    print(json.dumps(out), flush=True)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", f"r3_ref_replay_cfg{args.config}.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

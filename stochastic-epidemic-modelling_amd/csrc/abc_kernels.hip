@@ -13,7 +13,10 @@
 // passes integer days.  An event past day T-1 only changes row T, which :88 truncates away: the walk stops.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 #include "abc_device.hpp"
+#include "epipf_group.hpp"
 #include "epipf_internal.hpp"
 
 namespace epipf {
@@ -25,56 +28,76 @@ __device__ __forceinline__ void write_day(int32_t* col, size_t n, int d, double 
     p[2 * n] = (int32_t)R;
 }
 
+// Trial t's prior (abc_algo.py:35-36) and initial counts (:38-39): theta in cp, counts in x
+__device__ __forceinline__ void abc_trial_start(const AbcArgs& a, uint32_t t, ChainParam& cp, double* x) {
+    const Block rp = philox(0u, t, kDomainAbcPrior, a.f, a.k0, a.k1);
+    cp.theta[0] = a.prior_lo[0] + a.prior_rng[0] * u01(rp.x, rp.y);             // abc_algo.py:35
+    cp.theta[1] = a.prior_lo[1] + a.prior_rng[1] * u01(rp.z, rp.w);             // :36
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {                                               // :38-39
+        const Block r = philox((uint32_t)c, t, kDomainAbcInit, a.f, a.k0, a.k1);
+        x[c] = (double)poisson_mode_inversion(a.lam[c], u01(r.x, r.y), a.pm[c]);
+    }
+}
+
+// The trial's SIR path from x over [0, T-1] (gillespie_algo.py:10-75 with the reference-exact clock), writing each
+// day row as the clock passes it: day d holds the state after every event with time <= d.  `write`: this lane
+// stores the rows (the lane-group kernel runs it on every lane of a group, one of which writes).  Returns the events;
+// x holds the final state, day the first row not yet written, iters the loop iterations.
+__device__ __forceinline__ int abc_exact_path(double* x, const ChainParam& cp, uint32_t t, const AbcArgs& a,
+                                              const LogTab* __restrict__ tab, int32_t* col, bool write, int& day,
+                                              double& next_day, int& iters) {
+    const size_t n = (size_t)a.n;
+    SsaState<kSIR, 1> st;
+    st.load(x, cp);
+    const double R0 = x[2];
+    const double last_day = a.last_day;
+    double clock = 0.0;
+    uint32_t k = 0;
+    int nev = 0;
+    bool alive = st.active();
+    Block rn{0u, 0u, 0u, 0u};
+    if (alive) rn = philox(0u, t, kDomainAbcSsa, a.f, a.k0, a.k1);
+    while (alive) {                          // every lane enters at k = 0: k stays wave-uniform
+        const Block r = rn;
+        ++k;
+        rn = philox(__builtin_amdgcn_readfirstlane(k), t, kDomainAbcSsa, a.f, a.k0, a.k1);
+        const double S0 = st.S, I0 = st.I;
+        const int rec0 = st.nrec;
+        const bool ev = st.template event<true>(r, clock, last_day, cp, tab);   // false: the event lands after day T-1
+        if (ev) {
+            ++nev;
+            while (next_day < clock) {                                   // days the event does not reach
+                if (write) write_day(col, n, day, S0, I0, R0 + (double)rec0);
+                ++day;
+                next_day += 1.0;
+            }
+        }
+        alive = ev && st.active();
+    }
+    st.save(x);
+    iters = (int)k;
+    return nev;
+}
+
 __global__ __launch_bounds__(256) void abc_trials_kernel(AbcArgs a) {
     __shared__ LogTab tab[kLogTabEntries];
     if (threadIdx.x < kLogTabEntries) tab[threadIdx.x] = a.logtab[threadIdx.x];
     __syncthreads();
-    const int g = blockIdx.x * 256 + threadIdx.x;
+    const int g = a.g0 + (int)(blockIdx.x * 256 + threadIdx.x);    // sorted position (from g0: the lane groups below)
     int nev = 0, iters = 0;
     if (g < a.n) {
         const int i = a.perm ? a.perm[g] : g;
         const uint32_t t = a.t0 + (uint32_t)i;
         const size_t n = (size_t)a.n;
         ChainParam cp;
-        const Block rp = philox(0u, t, kDomainAbcPrior, a.f, a.k0, a.k1);
-        cp.theta[0] = a.prior_lo[0] + a.prior_rng[0] * u01(rp.x, rp.y);         // abc_algo.py:35
-        cp.theta[1] = a.prior_lo[1] + a.prior_rng[1] * u01(rp.z, rp.w);         // :36
         double x[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {                                           // :38-39
-            const Block r = philox((uint32_t)c, t, kDomainAbcInit, a.f, a.k0, a.k1);
-            x[c] = (double)poisson_mode_inversion(a.lam[c], u01(r.x, r.y), a.pm[c]);
-        }
-        SsaState<kSIR, 1> st;
-        st.load(x, cp);
-        const double R0 = x[2];
-        const double last_day = a.last_day;
+        abc_trial_start(a, t, cp, x);
         int32_t* col = a.days + i;
-        double clock = 0.0, next_day = 0.0;
         int day = 0;
-        uint32_t k = 0;
-        bool alive = st.active();
-        Block rn{0u, 0u, 0u, 0u};
-        if (alive) rn = philox(0u, t, kDomainAbcSsa, a.f, a.k0, a.k1);
-        while (alive) {                          // every lane enters at k = 0: k stays wave-uniform
-            const Block r = rn;
-            ++k;
-            rn = philox(__builtin_amdgcn_readfirstlane(k), t, kDomainAbcSsa, a.f, a.k0, a.k1);
-            const double S0 = st.S, I0 = st.I;
-            const int rec0 = st.nrec;
-            const bool ev = st.template event<true>(r, clock, last_day, cp, tab);   // false: the event lands after day T-1
-            if (ev) {
-                ++nev;
-                while (next_day < clock) {                               // days the event does not reach
-                    write_day(col, n, day, S0, I0, R0 + (double)rec0);
-                    ++day;
-                    next_day += 1.0;
-                }
-            }
-            alive = ev && st.active();
-        }
-        for (; day < a.T; ++day) write_day(col, n, day, st.S, st.I, R0 + (double)st.nrec);
-        iters = (int)k;
+        double next_day = 0.0;
+        nev = abc_exact_path(x, cp, t, a, tab, col, true, day, next_day, iters);
+        for (; day < a.T; ++day) write_day(col, n, day, x[0], x[1], x[2]);
         a.theta[i] = cp.theta[0];
         a.theta[n + i] = cp.theta[1];
     }
@@ -92,6 +115,79 @@ __global__ __launch_bounds__(256) void abc_trials_kernel(AbcArgs a) {
             atomicAdd(slot + 2, li);
             atomicAdd(slot + 3, 64ull * (unsigned long long)wmax);
         }
+    }
+}
+
+// Lane groups for the longest trials (round 3).  Sorted longest first, the first `group_end` trials are the
+// explosive epidemics (~10^4 events each, a quarter of the trials holding ~70% of the events at the reference's
+// setting): on one lane each they set the launch's length, a lone wave's dependent event loop.  Here W lanes run
+// one trial (epipf_group.hpp's group_propagate, the filter's lane-group SSA: bit-identical to the exact loop), the
+// day rows written by the lane that holds the state before each day-crossing event.  Concurrent with the one-lane
+// kernel over the rest (its own stream), which fills the SIMDs the groups leave idle.
+struct AbcDays {
+    static constexpr bool kOn = true;
+    int32_t* col;
+    size_t n;
+    int day;
+    double next_day;
+    bool lead;                                  // group lane 0: writes on the exact path and the tail rows
+    const AbcArgs* a;
+    // event at clock tt (<= T-1): the rows of the days before it hold the state before the event (owner: this lane)
+    template <class F>
+    __device__ __forceinline__ void passed(double tt, bool owner, const F& before, const double* x0) {
+        while (next_day < tt) {
+            if (owner) {
+                double xs[3] = {x0[0], x0[1], x0[2]};
+                before.save(xs);
+                write_day(col, n, day, xs[0], xs[1], xs[2]);
+            }
+            ++day;
+            next_day += 1.0;
+        }
+    }
+    // outside the f32 test's range: the one-lane kernel's exact loop, rows by the lead lane
+    __device__ __forceinline__ int exact(double* x, const ChainParam& cp, uint32_t t, uint32_t, double,
+                                         const LogTab* __restrict__ tab) {
+        int iters = 0;
+        return abc_exact_path(x, cp, t, *a, tab, col, lead, day, next_day, iters);
+    }
+};
+
+template <int W>
+__global__ __launch_bounds__(256) void abc_trials_group_kernel(AbcArgs a) {
+    __shared__ LogTab tab[kLogTabEntries];
+    if (threadIdx.x < kLogTabEntries) tab[threadIdx.x] = a.logtab[threadIdx.x];
+    __syncthreads();
+    const int gl = (int)(threadIdx.x & (W - 1));
+    const int g = (int)((blockIdx.x * 256 + threadIdx.x) / W);     // sorted position, one trial per group
+    int nev = 0;
+    if (g < a.group_end) {                                         // whole groups: group_end is per group
+        const int i = a.perm[g];
+        const uint32_t t = a.t0 + (uint32_t)i;
+        const size_t n = (size_t)a.n;
+        ChainParam cp{};
+        double x[3];
+        abc_trial_start(a, t, cp, x);
+        cp.thetaf[0] = (float)cp.theta[0];
+        cp.thetaf[1] = (float)cp.theta[1];
+        cp.f = a.f; cp.k0 = a.k0; cp.k1 = a.k1;
+        cp.flags = kChainFastSsa;
+        cp.clock_slack = 1.f;
+        AbcDays d{a.days + i, n, 0, 0.0, gl == 0, &a};
+        double xf[3];
+        nev = group_propagate<kSIR, 1, W, 1, AbcDays>(x, xf, cp, t, kDomainAbcSsa, a.last_day, tab, &d);
+        if (gl == 0) {
+            for (; d.day < a.T; ++d.day) write_day(d.col, n, d.day, xf[0], xf[1], xf[2]);
+            a.theta[i] = cp.theta[0];
+            a.theta[n + i] = cp.theta[1];
+        } else {
+            nev = 0;                                               // counted once per trial
+        }
+    }
+    if (a.count) {
+        unsigned long long e = (unsigned long long)nev;
+        for (int o = 32; o > 0; o >>= 1) e += __shfl_xor(e, o, 64);
+        if ((threadIdx.x & 63) == 0) atomicAdd(counter_slot(a.counters), e);
     }
 }
 
@@ -187,15 +283,33 @@ __global__ __launch_bounds__(256) void abc_gather_kernel(AbcGatherArgs a, int ma
     }
 }
 
-hipError_t launch_abc_trials(const AbcArgs& a, hipStream_t s) {
-    if (a.n <= 0) return hipSuccess;
+hipError_t launch_abc_trials(const AbcArgs& a0, hipStream_t s, hipStream_t s2, hipEvent_t fork, hipEvent_t join) {
+    if (a0.n <= 0) return hipSuccess;
+    AbcArgs a = a0;
+    a.g0 = 0;
     if (a.perm) {
         hipLaunchKernelGGL(abc_predict_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
         size_t bytes = a.sort_temp_bytes;
         hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(a.sort_temp, bytes, a.sort_keys[0], a.sort_keys[1],
                                                                     a.sort_vals[0], a.sort_vals[1], a.n, 0, 16, s);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(abc_trials_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+        const int ng = (a.group_lanes > 1 && s2) ? std::min(a.group_end, a.n) : 0;
+        if (ng > 0) {                           // the longest trials on lane groups, concurrently on s2
+            a.group_end = ng;
+            a.g0 = ng;
+            (void)hipEventRecord(fork, s);
+            (void)hipStreamWaitEvent(s2, fork, 0);
+            const unsigned blocks = (unsigned)(((long)ng * a.group_lanes + 255) / 256);
+            switch (a.group_lanes) {
+                case 2: hipLaunchKernelGGL(abc_trials_group_kernel<2>, dim3(blocks), dim3(256), 0, s2, a); break;
+                case 8: hipLaunchKernelGGL(abc_trials_group_kernel<8>, dim3(blocks), dim3(256), 0, s2, a); break;
+                default: hipLaunchKernelGGL(abc_trials_group_kernel<4>, dim3(blocks), dim3(256), 0, s2, a); break;
+            }
+            (void)hipEventRecord(join, s2);
+        }
+        if (a.n > a.g0)
+            hipLaunchKernelGGL(abc_trials_kernel, dim3((a.n - a.g0 + 255) / 256), dim3(256), 0, s, a);
+        if (ng > 0) (void)hipStreamWaitEvent(s, join, 0);
     } else {
         hipLaunchKernelGGL(abc_trials_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
     }

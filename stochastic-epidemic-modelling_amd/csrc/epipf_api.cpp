@@ -87,6 +87,10 @@ struct epipf_ctx {
     size_t abc_bytes = 0;
     void* abc = nullptr;
     bool abc_order = true;   // length-ordered ABC lanes (EPIPF_ABC_ORDER=0 disables)
+    // lanes per trial for the longest ABC trials: 0 = automatic (4 for launches of <= kAbcGroupMaxTrials trials,
+    // where the longest trials' lone waves set the launch's length; 1 above), EPIPF_ABC_LANES overrides (1 = off)
+    int abc_lanes = 0;
+    double abc_group_frac = 0.5, abc_frac = 0.5;   // share of the sorted trials on lane groups (EPIPF_ABC_GROUP_FRAC)
     bool fast_ssa = true;    // certified f32 event loop (EPIPF_SSA_FAST=0 disables; results are identical)
     float clock_slack = 1.f; // EPIPF_CLOCK_SLACK >= 1 widens its clock band: replays on purpose (stress tests)
     int n_streams = 4;   // chain groups on concurrent streams (EPIPF_STREAMS overrides, 1..kMaxFilterStreams)
@@ -722,6 +726,15 @@ int abc_prepare(epipf_ctx* c, const double* Y, int T, const double* priors, uint
     a.count = c->profiling >= EPIPF_PROFILE_COUNTERS ? 1 : 0;
     c->abc_order = true;
     if (const char* e = getenv("EPIPF_ABC_ORDER")) c->abc_order = atoi(e) != 0;
+    // lane groups for the longest trials (abc_trials_group_kernel): W lanes each for the first `abc_group_frac` of
+    // the sorted trials; EPIPF_ABC_LANES = 1 turns them off (results are identical either way)
+    a.group_lanes = c->abc_lanes;                                      // 0: chosen per launch (abc_launch_trials)
+    if (const char* e = getenv("EPIPF_ABC_LANES")) {
+        const int w = atoi(e);
+        if (w == 1 || w == 2 || w == 4 || w == 8) a.group_lanes = w;
+    }
+    c->abc_frac = c->abc_group_frac;
+    if (const char* e = getenv("EPIPF_ABC_GROUP_FRAC")) c->abc_frac = std::max(0.0, std::min(1.0, atof(e)));
     return 0;
 }
 
@@ -759,11 +772,23 @@ int abc_buffers(epipf_ctx* c, int T, int batch, int samples, AbcPlan& p) {
     return 0;
 }
 
-int abc_launch_trials(epipf_ctx* c, AbcArgs& a, uint32_t t0, int n) {
+// Launches of up to this many trials put the longest half on lane groups of 4 (automatic mode).  Measured at the
+// reference's setting (profiles/r3_abc_lane_groups.jsonl): 64k-trial launches 5.0 -> 3.1 ms (+61% end to end), 128k
+// +14%, 192k +3.5%, 256k (the default batch) no change -- from there the launch is throughput-bound and the groups'
+// extra instructions per event cancel what they save on the longest trials.
+constexpr int kAbcGroupMaxTrials = 196608;
+
+int abc_launch_trials(epipf_ctx* c, AbcArgs& a0, uint32_t t0, int n) {
+    AbcArgs& a = a0;
     a.t0 = t0;
     a.n = n;
+    const int lanes = a.group_lanes;
+    if (lanes == 0) a.group_lanes = n <= kAbcGroupMaxTrials ? 4 : 1;
+    a.group_end = (a.group_lanes > 1 && a.perm) ? (int)std::llround(c->abc_frac * n) : 0;
+    if (a.group_end > 0 && !ensure_streams(c, 2)) return fail(EPIPF_EHIP, "auxiliary stream creation failed");
     if (c->profiling) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-    hipError_t le = launch_abc_trials(a, c->stream);
+    hipError_t le = launch_abc_trials(a, c->stream, a.group_end > 0 ? c->aux[1] : nullptr, c->fork, c->join[1]);
+    a.group_lanes = lanes;                                             // automatic again for the next launch
     if (le != hipSuccess) return fail(EPIPF_EHIP, "ABC trial kernel launch failed: %s", hipGetErrorString(le));
     if (c->profiling) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     return 0;

@@ -125,9 +125,16 @@ __device__ __forceinline__ double exact_scale(const SsaState<MODEL, G>& ex, cons
 //   per lane: each kept state's 1/sum(a) (two IEEE divisions) times its -log(1 - U) = tau (SsaState::tau_of's
 //          expression);
 //   clock: t + tau in event order, stop at the first t + tau > tmax.
-template <int MODEL, int G, int W, int K>
+// Day recorder of the ABC trial (abc_kernels.hip): `days` is every event's clock in order, with the state before it.
+// The filter records nothing.
+struct NoDays {
+    static constexpr bool kOn = false;
+};
+
+template <int MODEL, int G, int W, int K, class Days = NoDays>
 __device__ __forceinline__ int group_propagate(const double* x0, double* xout, const ChainParam& cp, uint32_t j,
-                                               uint32_t ptag, double tmax, const LogTab* __restrict__ tab) {
+                                               uint32_t ptag, double tmax, const LogTab* __restrict__ tab,
+                                               Days* days = nullptr) {
     using F = FastSsa<MODEL, G>;
     constexpr int C = Shape<MODEL, G>::C;
     constexpr int E = W * K;
@@ -139,8 +146,12 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         // (same result in each); the lanes here all start at event 0 together, so its event index stays uniform
 #pragma unroll
         for (int c = 0; c < C; ++c) xout[c] = x0[c];
-        int it = 0;
-        return exact_propagate<MODEL, G>(xout, cp, j, ptag, tmax, tab, it);
+        if constexpr (Days::kOn) {
+            return days->exact(xout, cp, j, ptag, tmax, tab);
+        } else {
+            int it = 0;
+            return exact_propagate<MODEL, G>(xout, cp, j, ptag, tmax, tab, it);
+        }
     }
     // xout = the state s of group lane `own` (relative to the parent x0), in every lane of the group
     auto put = [&](const F& s, int own) __attribute__((always_inline)) {
@@ -231,6 +242,9 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
             tt = tt + __longlong_as_double(((uint64_t)hi << 32) | lo);
             alive = alive && !(tt > tmax);                   // :65-66
             inside += alive ? 1 : 0;
+            if constexpr (Days::kOn) {                       // event e happened at tt: days before it (rare)
+                if (alive && e < nk) days->passed(tt, gl == e % W, mine[e / W], x0);
+            }
             return true;
         };
         StaticFor<0, E>::run(clock);

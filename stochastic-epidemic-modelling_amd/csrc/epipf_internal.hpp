@@ -119,6 +119,8 @@ struct AbcArgs {
     const LogTab* logtab;
     const double* Y;             // [T][3] observed (S, I, R)
     int T, n, count;             // days, trials this launch, profiling counters on
+    int g0;                      // abc_trials_kernel: first sorted position it runs (the ones before: lane groups)
+    int group_end, group_lanes;  // the first group_end sorted trials on group_lanes lanes each (1: none)
     // length-ordered lanes (one lane per trial): predicted-length keys sorted with their trial offsets, lane g
     // runs trial perm[g].  NULL: lane g runs trial g.
     const int32_t* perm;
@@ -182,7 +184,7 @@ hipError_t launch_path_sample(const PathArgs& a, hipStream_t s);
 hipError_t launch_simulate(const SimArgs& a, int model, int G, hipStream_t s);
 hipError_t launch_simulate_path(const SimPathArgs& a, int model, int G, hipStream_t s);
 hipError_t launch_resample(const ResampleArgs& a, hipStream_t s);
-hipError_t launch_abc_trials(const AbcArgs& a, hipStream_t s);
+hipError_t launch_abc_trials(const AbcArgs& a, hipStream_t s, hipStream_t s2, hipEvent_t fork, hipEvent_t join);
 size_t abc_sort_temp_bytes(int n);
 hipError_t launch_abc_select(const AbcSelectArgs& a, hipStream_t s);
 hipError_t launch_abc_gather(const AbcGatherArgs& a, int max_count, hipStream_t s);

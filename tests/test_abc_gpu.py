@@ -141,3 +141,38 @@ def test_abc_large_run_properties(abc_golden, engine):
     np.testing.assert_array_equal(th[0], theta[-1])
     oth, orows, odist, _ = oracle.abc_trials(Y, pr, 2024, 3, trials - 1, 1)
     np.testing.assert_array_equal(orows[0], traj[-1, :, 1:].astype(np.int32))
+
+
+@pytest.mark.parametrize("lanes,frac", [(2, 0.25), (4, 0.25), (8, 0.25), (4, 1.0), (4, 0.003)])
+def test_abc_lane_groups_equal_one_lane_and_oracle(abc_golden, engine, monkeypatch, lanes, frac):
+    """The longest trials on lane groups (abc_trials_group_kernel, W lanes per trial, concurrent with the one-lane
+    kernel): theta, day tables and distances bit-identical to the one-lane kernel and to the oracle, for every
+    group width and share of the trials (all of them, a quarter, a handful)."""
+    rec = abc_golden["abc_noisy_150"]
+    n = 6000
+    out = {}
+    for w in (1, lanes):
+        monkeypatch.setenv("EPIPF_ABC_LANES", str(w))
+        monkeypatch.setenv("EPIPF_ABC_GROUP_FRAC", str(frac))
+        out[w] = engine.abc_trials(rec["Y"], priors_of(rec), 4242, 3, 1000, n)
+    for a, b in zip(out[1], out[lanes]):
+        np.testing.assert_array_equal(a, b)
+    oth, orows, odist, _ = oracle.abc_trials(rec["Y"], priors_of(rec), 4242, 3, 1000, n)
+    np.testing.assert_array_equal(out[lanes][0], oth)
+    np.testing.assert_array_equal(out[lanes][1], orows)
+    np.testing.assert_array_equal(out[lanes][2], odist)
+
+
+@pytest.mark.parametrize("name", ABC_CASES)
+def test_abc_lane_groups_reference_goldens(abc_golden, monkeypatch, name):
+    """The five reference ABC runs end to end with every trial on lane groups (share 1.0)."""
+    from epipf.abc import abc_run
+    monkeypatch.setenv("EPIPF_ABC_LANES", "4")
+    monkeypatch.setenv("EPIPF_ABC_GROUP_FRAC", "1.0")
+    rec = abc_golden["abc_" + name]
+    r = abc_run(rec["Y"], int(rec["n"]), float(rec["threshold"]), priors_of(rec), key=int(rec["key"]),
+                run_index=int(rec["f"]))
+    np.testing.assert_array_equal(r["beta"], rec["beta"])
+    np.testing.assert_array_equal(r["gamma"], rec["gamma"])
+    np.testing.assert_array_equal(r["trajectories"], rec["trajectories"])
+    assert r["trials"] == int(rec["trials"])
