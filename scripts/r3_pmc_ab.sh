@@ -8,7 +8,7 @@ ROOT=$(pwd)
 mkdir -p gpurun_out/pmcab
 for side in A B; do
   dir=$ROOT; [ $side = A ] && dir=$ROOT/ab_old
-  (cd $dir && timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_INSTS_LDS \
+  (cd $dir && timeout -s KILL 180 rocprofv3 --pmc ${PMC:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_INSTS_LDS} \
       --kernel-include-regex pf_step_kernel -d $ROOT/gpurun_out/pmcab/$side -o run --output-format csv -- \
       python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-single-chain) > gpurun_out/pmcab/$side.log 2>&1 \
       || { echo "STOP $side rc=$?"; tail -5 gpurun_out/pmcab/$side.log; exit 1; }

@@ -93,6 +93,7 @@ struct epipf_ctx {
     double abc_group_frac = 0.5, abc_frac = 0.5;   // share of the sorted trials on lane groups (EPIPF_ABC_GROUP_FRAC)
     bool fast_ssa = true;    // certified f32 event loop (EPIPF_SSA_FAST=0 disables; results are identical)
     float clock_slack = 1.f; // EPIPF_CLOCK_SLACK >= 1 widens its clock band: replays on purpose (stress tests)
+    double tie_scale = 1.0;  // EPIPF_TIE_SCALE >= 1 widens particle_weight's tie band: the all-columns pass on purpose
     int n_streams = 4;   // chain groups on concurrent streams (EPIPF_STREAMS overrides, 1..kMaxFilterStreams)
     hipStream_t aux[kMaxFilterStreams] = {};
     hipEvent_t join[kMaxFilterStreams] = {};
@@ -222,6 +223,7 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     c->wg = default_wg(n_particles);
     if (const char* e = getenv("EPIPF_SSA_FAST")) c->fast_ssa = atoi(e) != 0;
     if (const char* e = getenv("EPIPF_CLOCK_SLACK")) c->clock_slack = std::max(1.0f, std::min(1e6f, (float)atof(e)));
+    if (const char* e = getenv("EPIPF_TIE_SCALE")) c->tie_scale = std::max(1.0, std::min(1e300, atof(e)));
     if (const char* e = getenv("EPIPF_STREAMS")) c->n_streams = std::max(1, std::min(kMaxFilterStreams, atoi(e)));
     if (const char* e = getenv("EPIPF_LANES")) {
         const int w = atoi(e);
@@ -366,7 +368,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
         // an ulp of the sum of their terms' magnitudes, 2 log n! + n (|log p| + |log1p(-p)|) at n = the population
         const double nmax = (double)std::max(c->lf_max, 0);
         q.tie_tol = (2.0 * std::lgamma(nmax + 1.0) * 1.01 + nmax * (std::fabs(q.logp) + std::fabs(q.log1mp)) + 1.0) *
-                    0x1.0p-46;
+                    0x1.0p-46 * c->tie_scale;
         q.k0 = (uint32_t)keys[ch];
         q.k1 = (uint32_t)(keys[ch] >> 32);
         q.f = filter_index[ch];

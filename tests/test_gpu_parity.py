@@ -626,3 +626,54 @@ def test_full_size_baseline_configs_vs_oracle(cfg, chains, lanes, streams, check
           f"{stats['resample_ref_ambiguous']} reference-ambiguous draws of {chains * N * (Y.shape[0] - 1)}")
     assert bad == 0
     assert stats["resample_ref_ambiguous"] <= 3
+
+
+def test_weight_tie_path_equals_oracle(datasets_golden, monkeypatch):
+    """particle_weight's all-columns pass (binom_weight_tied, normally ~1e-6 of particle-steps) forced for every
+    particle (EPIPF_TIE_SCALE widens the tie band to everything): SIR, SEIR and both subgroup models stay bit-exact to
+    the oracle -- the out-of-line pass computes the same compensated minimum."""
+    from epipf.engine import Engine, model_id, theta_vector
+    monkeypatch.setenv("EPIPF_TIE_SCALE", "1e300")
+    cases = [("sir", datasets_golden["sir_binom"], (2.0, 1.0), 4820.0, 20.0),
+             ("seir", datasets_golden["seir_binom"], (4.0, 1.0, 1.0), 4820.0, 20.0),
+             ("sir_subgroups", datasets_golden["sub_binom"][:6], (np.array([[5.0, 2.0], [1.0, 3.0]]), 0.5),
+              np.array([2030.0, 3040.0]), np.array([30.0, 40.0])),
+             ("sir_subgroups2", datasets_golden["sub2_binom"][:6], (np.array([[5.0, 2.0], [1.0, 3.0]]), 0.5),
+              np.array([2030.0, 3040.0]), np.array([30.0, 40.0]))]
+    for model, Y, th, npop, mu in cases:
+        mid = model_id(model)
+        thv, G = theta_vector(mid, th)
+        for lanes in (1, 0):
+            eng = Engine(model, G, 700, Y.shape[0], 1)        # created after the env: it reads EPIPF_TIE_SCALE
+            eng.set_observations(Y)
+            eng.set_population(npop, mu)
+            eng.set_lanes(lanes)
+            lz, st = eng.run(thv[None], [0.1], [55], [2])
+            hid, anc = eng.history(1)
+            eng.close()
+            o = oracle.particle_filter(Y, model, th, False, 0.1, 700, npop, mu, key=55, filter_index=2)
+            assert int(st[0]) == o["status"] == 0, (model, lanes)
+            np.testing.assert_array_equal(hid[0], o["hidden"], err_msg=f"{model} lanes {lanes}")
+            np.testing.assert_array_equal(anc[0], o["ancestry"], err_msg=f"{model} lanes {lanes}")
+            np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
+def test_large_population_weights_vs_oracle():
+    """A population of 2*10^5: the binary128 log-factorial table is built by several host threads (above 64k entries)
+    and the weights' counts reach 10^5; bit-exact states and ancestors vs the oracle (single-threaded table)."""
+    from epipf.engine import Engine
+    rs = np.random.RandomState(8)
+    T, npop = 6, 200000.0
+    th = (0.02, 0.01)                                  # a slow epidemic: ~30 events per particle-step
+    Y = np.floor(0.1 * np.array([[199400.0, 600.0, 0.0]] * T)) + rs.randint(-20, 20, (T, 3)) * [1, 0, 0]
+    eng = Engine("sir", 1, 900, T, 1)
+    eng.set_observations(Y)
+    eng.set_population(npop, 600.0)
+    lz, st = eng.run(np.array([th]), [0.1], [9], [1])
+    hid, anc = eng.history(1)
+    eng.close()
+    o = oracle.particle_filter(Y, "sir", th, False, 0.1, 900, npop, 600.0, key=9, filter_index=1)
+    assert int(st[0]) == o["status"] == 0
+    np.testing.assert_array_equal(hid[0], o["hidden"])
+    np.testing.assert_array_equal(anc[0], o["ancestry"])
+    np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
