@@ -868,40 +868,38 @@ __device__ __forceinline__ void fast_two_sum(double a, double b, double& s, doub
 
 // The log-factorial table: lf[n] = hi and lf[lf_max + 1 + n] = lo of log n!, n = 0..lf_max (binary128 split on the
 // host, logfact.cpp).  Hi and lo apart: the ranking pass reads only the hi parts (the table footprint in L1/L2 of
-// the old plain weight), and the lo parts of the minimum's three entries are read once it is known.
+// the old plain weight); the minimum's three entries are read again, hi and lo, once it is known (L1 hits).
 struct LfIdx { int n, k, m; };
 
-// Plain-double log pmf from the hi parts (the candidate ranking of particle_weight; -inf / NaN as LogW.hi), plus
-// what the compensated value needs: s2 = (log n! - log k!) - log (n-k)! in hi parts (the plain sum's own first two
-// additions), e12 = those two additions' exact rounding errors, and the entries' indices.  log n! >= log k! and
-// log(n!/k!) >= log (n-k)! (n!/k! is a product of n-k factors each >= its counterpart in (n-k)!), so both are fast
-// two-sums.
+__device__ __forceinline__ LfIdx lf_index(double k, double n, int lf_max) {
+    const int ni = min(max((int)n, 0), lf_max), ki = min(max((int)k, 0), lf_max);
+    return LfIdx{ni, ki, min(max(ni - ki, 0), lf_max)};
+}
+
+// Plain-double log pmf from the hi parts: the candidate ranking of particle_weight (-inf / NaN as LogW.hi).
 __device__ __forceinline__ double binom_logpmf_plain(double k, double n, const ChainParam& cp, const double* lf,
-                                                     int lf_max, double& s2, double& e12, LfIdx& ix) {
-    s2 = e12 = 0.0;
-    ix = LfIdx{0, 0, 0};
+                                                     int lf_max) {
     const double p = cp.probs;
     if (!(p >= 0.0 && p <= 1.0)) return __builtin_nan("");
     if (k < 0.0 || k > n || k != floor(k)) return -__builtin_inf();
     if (p == 0.0) return (k == 0.0) ? 0.0 : -__builtin_inf();
     if (p == 1.0) return (k == n) ? 0.0 : -__builtin_inf();
-    const int ni = min(max((int)n, 0), lf_max), ki = min(max((int)k, 0), lf_max);
-    ix = LfIdx{ni, ki, min(max(ni - ki, 0), lf_max)};
-    double s1, e1, e2;
-    fast_two_sum(lf[ix.n], -lf[ix.k], s1, e1);
-    fast_two_sum(s1, -lf[ix.m], s2, e2);
-    e12 = e1 + e2;
-    return s2 + (k * cp.logp + (n - k) * cp.log1mp);
+    const LfIdx ix = lf_index(k, n, lf_max);
+    return ((lf[ix.n] - lf[ix.k]) - lf[ix.m]) + (k * cp.logp + (n - k) * cp.log1mp);
 }
 
-// The compensated log pmf of a regular case (0 < p < 1, k integral in [0, n]) from binom_logpmf_plain's outputs:
-// the table's lo parts, the products' exact errors (fma), an exact two-sum of the products and one of the total, the
-// lo terms summed in double.
-__device__ __forceinline__ LogW binom_logpmf_core(double k, double n, double s2, double e12, LfIdx ix,
-                                                  const double* lf, int lf_max, double logp, double log1mp,
-                                                  double logp_lo, double log1mp_lo) {
+// The compensated log pmf of a regular case (0 < p < 1, k integral in [0, n]): the plain value's two factorial
+// differences as exact fast two-sums (log n! >= log k!, and log(n!/k!) >= log (n-k)!: n!/k! is a product of n-k
+// factors each >= its counterpart in (n-k)!), the table's lo parts, the products' exact errors (fma), an exact
+// two-sum of the products and one of the total, the lo terms summed in double.
+__device__ __forceinline__ LogW binom_logpmf_core(double k, double n, const double* lf, int lf_max, double logp,
+                                                  double log1mp, double logp_lo, double log1mp_lo) {
+    const LfIdx ix = lf_index(k, n, lf_max);
     const double* lo_tab = lf + lf_max + 1;
-    const double lt = ((lo_tab[ix.n] - lo_tab[ix.k]) - lo_tab[ix.m]) + e12;
+    double s1, e1, s2, e2;
+    fast_two_sum(lf[ix.n], -lf[ix.k], s1, e1);
+    fast_two_sum(s1, -lf[ix.m], s2, e2);
+    const double lt = ((lo_tab[ix.n] - lo_tab[ix.k]) - lo_tab[ix.m]) + (e1 + e2);
     const double m = n - k;
     double s3, e3, s4, e4;
     const double p1 = k * logp, f1 = fma(k, logp, -p1);               // exact products: p + f = k * logp
@@ -916,12 +914,10 @@ __device__ __forceinline__ LogW binom_logpmf_core(double k, double n, double s2,
 
 // the compensated log pmf with scipy's special cases (lo = 0 there)
 __device__ __forceinline__ LogW binom_logpmf(double k, double n, const ChainParam& cp, const double* lf, int lf_max) {
-    double s2, e12;
-    LfIdx ix;
-    const double h = binom_logpmf_plain(k, n, cp, lf, lf_max, s2, e12, ix);
+    const double h = binom_logpmf_plain(k, n, cp, lf, lf_max);
     const double p = cp.probs;
     if (!(h > -__builtin_inf()) || p == 0.0 || p == 1.0) return LogW{h, 0.0};   // NaN, pmf 0, or pmf 0 / 1 cases
-    return binom_logpmf_core(k, n, s2, e12, ix, lf, lf_max, cp.logp, cp.log1mp, cp.logp_lo, cp.log1mp_lo);
+    return binom_logpmf_core(k, n, lf, lf_max, cp.logp, cp.log1mp, cp.logp_lo, cp.log1mp_lo);
 }
 
 // a < b for compensated logs of nearby size (hi - hi is exact within a factor 2, Sterbenz); -inf and NaN by hi
@@ -961,16 +957,22 @@ __device__ __forceinline__ double observed(const double* x, int i) {
 template <int MODEL, int G>
 __device__ __attribute__((noinline)) double binom_weight_tied(const int32_t* row, const double* yrow,
                                                               const ChainParam* cpp, const double* lf, int lf_max) {
-    constexpr int K = Shape<MODEL, G>::K, C = Shape<MODEL, G>::C;
+    // a rolled loop reading the state from memory: this function's registers count towards the calling kernel's
+    // allocation (an unrolled 6- or 12-column version cost the subgroup step kernels two waves per SIMD)
+    constexpr int K = Shape<MODEL, G>::K;
     const ChainParam& cp = *cpp;
-    double x[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) x[c] = (double)row[c];
-    LogW L = binom_logpmf(yrow[0], observed<MODEL, G>(x, 0), cp, lf, lf_max);
-#pragma unroll
-    for (int i = 1; i < K; ++i) {
-        const LogW li = binom_logpmf(yrow[i], observed<MODEL, G>(x, i), cp, lf, lf_max);
-        if (logw_less(li, L)) L = li;
+    LogW L{0.0, 0.0};
+#pragma unroll 1
+    for (int i = 0; i < K; ++i) {
+        double xo;
+        if constexpr (MODEL == kSubgroups2) {
+            xo = 0.0;
+            for (int g = 0; g < G; ++g) xo = xo + (double)row[3 * g + i];     // group sum, pmcmc.py:173,229
+        } else {
+            xo = (double)row[i];
+        }
+        const LogW li = binom_logpmf(yrow[i], xo, cp, lf, lf_max);
+        if (i == 0 || logw_less(li, L)) L = li;
     }
     const double e = exp(L.hi);
     return fma(e, L.lo, e);
@@ -1003,33 +1005,28 @@ __device__ __forceinline__ double particle_weight(const double* x, const double*
     } else {
         asm volatile("" ::: "memory");
         const double logp_lo = cpp->logp_lo, log1mp_lo = cpp->log1mp_lo, tie_tol = cpp->tie_tol;
-        double lh[K];
-        double m = 0.0, ys = 0.0, xs = 0.0, s2m = 0.0, e12m = 0.0;   // the running minimum and its operands
-        LfIdx ixm{0, 0, 0};
+        // the running minimum m with its operands, and the runner-up m2 (a near tie: m2 - m <= tie_tol); NaN sticks.
+        // Only these four doubles live across the columns: keeping each column's table parts for a later select
+        // raised the subgroup kernels' registers by a third (75 -> 111 VGPRs at G = 2, two waves per SIMD fewer).
+        double m = 0.0, m2 = __builtin_inf(), ys = 0.0, xs = 0.0;
+        bool nan = false;
 #pragma unroll
         for (int i = 0; i < K; ++i) {
             const double xo = observed<MODEL, G>(x, i);
-            double s2, e12;
-            LfIdx ix;
-            lh[i] = binom_logpmf_plain(yrow[i], xo, cp, lf, lf_max, s2, e12, ix);
-            const bool take = (i == 0 || isnan(lh[i])) || (!isnan(m) && lh[i] < m);
-            m = take ? lh[i] : m;
+            const double h = binom_logpmf_plain(yrow[i], xo, cp, lf, lf_max);
+            nan = nan || isnan(h);
+            const bool take = (i == 0) || h < m;
+            m2 = (i == 0) ? m2 : (take ? m : fmin(m2, h));
+            m = take ? h : m;
             ys = take ? yrow[i] : ys;
             xs = take ? xo : xs;
-            s2m = take ? s2 : s2m;
-            e12m = take ? e12 : e12m;
-            ixm.n = take ? ix.n : ixm.n;
-            ixm.k = take ? ix.k : ixm.k;
-            ixm.m = take ? ix.m : ixm.m;
         }
-        if (isnan(m)) return m;                                        // np.min propagates NaN
+        if (nan) return __builtin_nan("");                             // np.min propagates NaN
         if (!(m > -__builtin_inf())) return 0.0;                       // a column outside its support: pmf 0
         if (cp.probs == 0.0 || cp.probs == 1.0) return 1.0;            // m finite: every column's pmf is 1
-        int below = 0;                                                 // columns within tie_tol of the minimum
-#pragma unroll
-        for (int i = 0; i < K; ++i) below += (lh[i] - m <= tie_tol) ? 1 : 0;
+        const int below = (m2 - m <= tie_tol) ? 2 : 1;                 // another column within tie_tol of m
         if (below > 1) return binom_weight_tied<MODEL, G>(row, yrow, cpp, lf, lf_max);
-        const LogW L = binom_logpmf_core(ys, xs, s2m, e12m, ixm, lf, lf_max, cp.logp, cp.log1mp, logp_lo, log1mp_lo);
+        const LogW L = binom_logpmf_core(ys, xs, lf, lf_max, cp.logp, cp.log1mp, logp_lo, log1mp_lo);
         const double e = exp(L.hi);
         return fma(e, L.lo, e);                                        // exp(hi + lo) = exp(hi) (1 + lo)
     }
