@@ -414,10 +414,11 @@ def main():
             "ssa_lane_utilisation": lane_use if lanes == 1 else None,
             "lanes_per_particle": lanes,
             "resample_fallbacks": st["resample_fallbacks"],
-            # draws of the timed region whose uniform lies within scipy's error envelope of a CDF boundary: the only
-            # draws where the reference's own weights could pick another ancestor; of all draws
-            "resample_ref_ambiguous": st["resample_ref_ambiguous"],
-            "resample_draws": filters * N * (T - 1),
+            # draws of the untimed counters iteration whose uniform lies within scipy's error envelope of a CDF
+            # boundary: the only draws where the reference's own weights could pick another ancestor;
+            # of that iteration's resampling draws (the test runs with the device counters only)
+            "resample_ref_ambiguous": cst["resample_ref_ambiguous"],
+            "resample_draws": cst["particle_steps"] * (T - 1) // T,
             "library_build_id": _lib.build_id(),
             "pmc_profile": {"build_id": pmc.get("build_id"), "current": pmc_current},
             "events_per_particle_step": cst["events"] / cst["particle_steps"] if cst["particle_steps"] else None,
