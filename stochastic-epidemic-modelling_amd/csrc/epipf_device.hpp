@@ -454,6 +454,13 @@ struct FastSsa<kSIR, 1> {                                              // gilles
         S = S - (ch == 0 ? s : 0.f);
         I = I + (ch == 0 ? s : -s);
     }
+    // the event from the wave masks below[i] of the certified sides c_i < U total (the lane-group pass,
+    // epipf_group.hpp: decide_flagged); the selects take the masks as their SGPR conditions
+    __device__ __forceinline__ void apply_below(const uint64_t* below) {
+        const bool rec = __builtin_amdgcn_inverse_ballot_w64(below[0]);
+        S = S - (rec ? 0.f : 1.f);
+        I = I + (rec ? -1.f : 1.f);
+    }
     __device__ __forceinline__ int save(double* x) const {
         const float inf = S0 - S, rec = SI0 - (S + I);
         x[0] = (double)S; x[1] = (double)I; x[2] = x[2] + (double)rec;
@@ -492,6 +499,12 @@ struct FastSsa<kSEIR, 1> {                                             // gilles
         S = S - (ch == 0 ? s : 0.f);
         E = E + (ch == 0 ? s : (ch == 1 ? -s : 0.f));
         I = I + (ch == 1 ? s : (ch == 2 ? -s : 0.f));
+    }
+    __device__ __forceinline__ void apply_below(const uint64_t* below) {   // below[1] implies below[0]
+        const bool b0 = __builtin_amdgcn_inverse_ballot_w64(below[0]), b1 = __builtin_amdgcn_inverse_ballot_w64(below[1]);
+        S = S - (b0 ? 0.f : 1.f);
+        E = E + (b0 ? (b1 ? 0.f : -1.f) : 1.f);
+        I = I + (b1 ? -1.f : (b0 ? 1.f : 0.f));
     }
     __device__ __forceinline__ int save(double* x) const {
         const float n0 = S0 - S, n2 = SEI0 - ((S + E) + I), n1 = (I - I0) + n2;
@@ -593,8 +606,170 @@ struct FastSubgroups {                                                 // gilles
         return (int)(inf + rec);
     }
 };
+// The subgroup model's f32 state in the lane-group pass (epipf_group.hpp), FastSubgroups' arithmetic with the
+// counts in pairs of groups (S[q] = S2[q / 2][q % 2]; an odd G's pad slot stays 0): the propensity products and the
+// state updates are packed f32 (v_pk_mul_f32 / v_pk_add_f32), one instruction per pair, and the event is applied
+// from the decision's wave masks (apply_below).  Same roundings per term as FastSubgroups (the same e_as and band).
+template <int G>
+struct FastSubgroupsPacked {                                           // gillespie_algo.py:148-233
+    static constexpr int NCH = G * G + G;
+    static constexpr float kBand = (2 * (4 + NCH) + 7 <= 32) ? 0x1.0p-19f : 0x1.0p-18f;   // (e_q + 2) ulp
+    static constexpr float kClockT = (float)(NCH + 11) * kUlpF;        // e_as = 4 + NCH
+    using f2 = float __attribute__((ext_vector_type(2)));
+    static constexpr int P = (G + 1) / 2;
+    double sumN;
+    f2 S2[P], I2[P];
+    f2 bN2[G][P];                                                      // beta[q][q2] / sum(N)
+    float Ng[G], S0sum, R0sum;
+    const float* b;                                                    // beta[G][G] then gamma, f32 (SGPRs)
+    // packed multiply (the selector scalarises a <2 x float> product whose halves are used apart); rounds each half
+    // as v_mul_f32
+    static __device__ __forceinline__ f2 pk_mul(f2 a, f2 b) {
+        f2 r;
+        asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+        return r;
+    }
+    __device__ __forceinline__ float S(int q) const { return S2[q >> 1][q & 1]; }
+    __device__ __forceinline__ float I(int q) const { return I2[q >> 1][q & 1]; }
+    __device__ __forceinline__ bool load(const double* x, const ChainParam& cp) {
+        sumN = 0.0;
+        bool ok = true;
+        S0sum = 0.f;
+        R0sum = 0.f;
+#pragma unroll
+        for (int p = 0; p < P; ++p) S2[p] = I2[p] = f2{0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+            sumN = sumN + ((x[3 * q] + x[3 * q + 1]) + x[3 * q + 2]);  // sum(N), :176,:182
+            S2[q >> 1][q & 1] = (float)x[3 * q];
+            I2[q >> 1][q & 1] = (float)x[3 * q + 1];
+            Ng[q] = (S(q) + I(q)) + (float)x[3 * q + 2];
+            S0sum += S(q);
+            R0sum += (float)x[3 * q + 2];
+        }
+        b = cp.thetaf;
+#pragma unroll
+        for (int q = 0; q <= G * G; ++q) ok = ok && rate_ok(b[q]);
+        // beta / sum(N) once per step (VGPR pairs, for the packed products).  Each term's error is that of
+        // (beta S)(I / sum(N)): four roundings before the accumulating fma (e_as unchanged).
+        const float invN = (float)(1.0 / sumN);
+#pragma unroll
+        for (int q = 0; q < G; ++q)
+#pragma unroll
+            for (int q2 = 0; q2 < 2 * P; ++q2) bN2[q][q2 >> 1][q2 & 1] = q2 < G ? b[q * G + q2] * invN : 0.f;
+        return ok && sumN >= 1.0 && sumN < 16777216.0;
+    }
+    __device__ __forceinline__ bool active() const {                   // :192-193, :222 (counts are >= 0)
+        float inf = I(0);
+#pragma unroll
+        for (int q = 1; q < G; ++q) inf = inf + I(q);
+        return inf > 0.f;
+    }
+    __device__ __forceinline__ float cum(float* c) const {             // channel order, :180-185
+        float run = 0.f;
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                const f2 bs = pk_mul(bN2[q][p], S2[p]);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int q2 = 2 * p + h;
+                    if (q2 < G) {
+                        run = fmaf(bs[h], I(q), run);
+                        if (q * (G + 1) + q2 < NCH - 1) c[q * (G + 1) + q2] = run;
+                    }
+                }
+            }
+            run = fmaf(b[G * G], I(q), run);
+            if (q * (G + 1) + G < NCH - 1) c[q * (G + 1) + G] = run;
+        }
+        return run;
+    }
+    __device__ __forceinline__ int exact_channel(const ChainParam& cp, double u) const {
+        double Sd[G], Id[G];
+#pragma unroll
+        for (int q = 0; q < G; ++q) { Sd[q] = (double)S(q); Id[q] = (double)I(q); }
+        return subgroups_channel_exact<G>(cp.theta, Sd, Id, sumN, u);
+    }
+    // Channel ch = g*(G+1) + c: c < G is infection s_{g}_{c} (S[c] -> I[c], :183), c = G recovery i_{g} (I[g] -> R,
+    // :185).  Only one group moves, q = c or g: a per-group select instead of a branch per channel (the compiler
+    // turns the channel-by-channel form into a divergent switch).  Whether ch is an infection and the group q it
+    // moves are bit fields of compile-time masks (one bit-field extract each, no division by G + 1).
+    static constexpr uint32_t chan_mask(int what) {      // what = -1: infection bits; 0/1: bit `what` of q
+        uint32_t m = 0;
+        for (int ch = 0; ch < NCH; ++ch) {
+            const int g = ch / (G + 1), c = ch % (G + 1), q = c < G ? c : g;
+            const bool bit = what < 0 ? c < G : ((q >> what) & 1) != 0;
+            m |= bit ? (1u << ch) : 0u;
+        }
+        return m;
+    }
+    static constexpr uint32_t kInfMask = chan_mask(-1), kQ0 = chan_mask(0), kQ1 = chan_mask(1);
+    __device__ __forceinline__ void apply(int ch, float s) {
+        static_assert(NCH <= 32 && G <= 4, "channel masks");
+        const bool inf = ((kInfMask >> ch) & 1u) != 0u;
+        const int q = (int)((kQ0 >> ch) & 1u) | (G > 2 ? (int)(((kQ1 >> ch) & 1u) << 1) : 0);
+        const float dS = inf ? s : 0.f, dI = inf ? s : -s;
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            f2 ds, di;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const bool hit = q == 2 * p + h;
+                ds[h] = hit ? dS : 0.f;
+                di[h] = hit ? dI : 0.f;
+            }
+            S2[p] = S2[p] - ds;
+            I2[p] = I2[p] + di;
+        }
+    }
+    // the event from the wave masks below[i] of the certified sides c_i < U total: channel ch happened iff below[ch - 1]
+    // and not below[ch] (the c_i are nondecreasing); group r gains an infection from channels g (G + 1) + r and loses
+    // one to recovery from channel r (G + 1) + G.  The mask logic is SALU; selects on the masks, one packed add per
+    // pair of counts.
+    __device__ __forceinline__ void apply_below(const uint64_t* below) {
+        auto hit = [&](int ch) __attribute__((always_inline)) -> uint64_t {
+            return (ch == 0 ? ~0ull : below[ch - 1]) & (ch == NCH - 1 ? ~0ull : ~below[ch]);
+        };
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            f2 ds{0.f, 0.f}, di{0.f, 0.f};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int r = 2 * p + h;
+                if (r < G) {
+                    uint64_t inf = 0;
+#pragma unroll
+                    for (int g = 0; g < G; ++g) inf |= hit(g * (G + 1) + r);
+                    const bool fi = __builtin_amdgcn_inverse_ballot_w64(inf);
+                    const bool fr = __builtin_amdgcn_inverse_ballot_w64(hit(r * (G + 1) + G));
+                    ds[h] = fi ? 1.f : 0.f;
+                    di[h] = fi ? 1.f : (fr ? -1.f : 0.f);
+                }
+            }
+            S2[p] = S2[p] - ds;
+            I2[p] = I2[p] + di;
+        }
+    }
+    __device__ __forceinline__ int save(double* x) const {
+        float inf = S0sum, rec = -R0sum;
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+            const float R = (Ng[q] - S(q)) - I(q);
+            inf -= S(q);
+            rec += R;
+            x[3 * q] = (double)S(q); x[3 * q + 1] = (double)I(q); x[3 * q + 2] = (double)R;
+        }
+        return (int)(inf + rec);
+    }
+};
 template <int G> struct FastSsa<kSubgroups, G> : FastSubgroups<G> {};
 template <int G> struct FastSsa<kSubgroups2, G> : FastSubgroups<G> {};
+// the f32 state of the lane-group pass
+template <int MODEL, int G> struct GroupSsa { using type = FastSsa<MODEL, G>; };
+template <int G> struct GroupSsa<kSubgroups, G> { using type = FastSubgroupsPacked<G>; };
+template <int G> struct GroupSsa<kSubgroups2, G> { using type = FastSubgroupsPacked<G>; };
 
 template <int MODEL, int G>
 __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,

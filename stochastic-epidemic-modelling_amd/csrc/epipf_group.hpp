@@ -77,25 +77,29 @@ __device__ __forceinline__ double group_lane_f64(double v) {
     return __longlong_as_double(((uint64_t)hi << 32) | lo);
 }
 
-// Channel decision of one event on the f32 state without the exact fallback: the certified test in its product form
-// (c_i against T = uc * total, the band scaled by total: within the band of every model, FastSsa / DESIGN.md §4),
-// with `close` raised when the test cannot certify (the caller then redoes the chunk on the exact fallback).  No
-// branch: the lane-group pass runs it once per event on its critical path.
+// Channel decision of one event on the f32 state without the exact fallback, applied to st.  The certified test
+// brackets U total: with ulo = uc - kBand (exact: uc is an odd multiple of 2^-24 below 1 and kBand a power of two
+// >= 2^-19), Tlo = fl(ulo total) and Thi = fl(Tlo + 2 kBand total), c_i < Tlo puts channel i's cumulative rate
+// certainly below U total and c_i >= Thi certainly above: the product form's band (FastSsa) less one
+// ulp of total for the two roundings, inside kBand's margin over 2 e_as + 2 ulp.  A lane of a live particle with
+// some c_i in between raises its bit of `close` (the caller then redoes the chunk on the exact fallback).  The
+// comparisons are taken as wave masks: the decision, its certificate and `close` are SALU logic, and the state
+// update is two or three selects per count on those masks (FastSsa::apply_below).  No branch: the lane-group pass
+// runs this once per event on its critical path.
 template <typename F>
-__device__ __forceinline__ int channel_flagged(const F& st, float uc, bool& close) {
+__device__ __forceinline__ void decide_flagged(F& st, float ulo, uint64_t& close) {
     constexpr int NCH = F::NCH;
     float c[NCH - 1];
     const float total = st.cum(c);
-    const float T = uc * total, band = F::kBand * total;
-    int ch = 0;
-    bool sure = true;
+    const float Tlo = ulo * total, Thi = fmaf(2.0f * F::kBand, total, Tlo);
+    uint64_t below[NCH - 1], unsure = 0;
 #pragma unroll
     for (int i = 0; i < NCH - 1; ++i) {
-        ch += (c[i] < T) ? 1 : 0;
-        sure = sure && (fabsf(c[i] - T) > band);
+        below[i] = __ballot(c[i] < Tlo);
+        unsure |= below[i] ^ __ballot(c[i] < Thi);
     }
-    close = close || (st.active() && !sure);
-    return ch;
+    close |= unsure & __ballot(st.active());
+    st.apply_below(below);
 }
 
 // 1/sum(a) of the exact state (the reference's expressions, SsaState::rates)
@@ -119,7 +123,7 @@ __device__ __forceinline__ double exact_scale(const SsaState<MODEL, G>& ex, cons
 //
 // Chunk of E = W K events, event e drawn by lane e % W in its slot e / W:
 //   per lane, independent of the state: K Philox blocks, their channel uniforms uc and -log(1 - U) (glibc's log);
-//   pass: E channel decisions in order, branch-free (channel_flagged); lane e % W keeps the state before event e;
+//   pass: E channel decisions in order, branch-free (decide_flagged); lane e % W keeps the state before event e;
 //   after: the first event whose state is extinct (ballots) -> events in the chunk; if any decision was not
 //          certified, the pass is redone with the exact fallback per event;
 //   per lane: each kept state's 1/sum(a) (two IEEE divisions) times its -log(1 - U) = tau (SsaState::tau_of's
@@ -135,7 +139,7 @@ template <int MODEL, int G, int W, int K, class Days = NoDays>
 __device__ __forceinline__ int group_propagate(const double* x0, double* xout, const ChainParam& cp, uint32_t j,
                                                uint32_t ptag, double tmax, const LogTab* __restrict__ tab,
                                                Days* days = nullptr) {
-    using F = FastSsa<MODEL, G>;
+    using F = typename GroupSsa<MODEL, G>::type;
     constexpr int C = Shape<MODEL, G>::C;
     constexpr int E = W * K;
     const int lane = (int)(threadIdx.x & 63);
@@ -172,21 +176,21 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
     F mine[K];                                           // mine[k]: state before event k W + gl
     for (;;) {
         Block r[K];
-        float uc[K];
+        float ulo[K];
         double L[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             r[k] = philox(base + (uint32_t)(k * W + gl), j, ptag, cp.f, cp.k0, cp.k1);
-            uc[k] = __uint_as_float(0x3F800000u | (r[k].w >> 9)) - (1.0f - kUlpF);       // uf + 2^-24
+            const float uc = __uint_as_float(0x3F800000u | (r[k].w >> 9)) - (1.0f - kUlpF);   // uf + 2^-24
+            ulo[k] = uc - F::kBand;
             L[k] = neg_log_one_minus_u01<true>(r[k].x, r[k].y, tab);                     // -log(1 - U), :62
         }
         const F st0 = st;
-        bool close = false;
+        uint64_t close = 0;                              // lanes whose decision did not certify
         auto decide = [&](auto I) __attribute__((always_inline)) -> bool {
             constexpr int e = decltype(I)::value;
             if (gl == e % W) mine[e / W] = st;
-            const float u = __uint_as_float(group_lane_dpp<W, e % W>(__float_as_uint(uc[e / W])));
-            st.apply(channel_flagged(st, u, close), 1.f);
+            decide_flagged(st, __uint_as_float(group_lane_dpp<W, e % W>(__float_as_uint(ulo[e / W]))), close);
             return true;
         };
         StaticFor<0, E>::run(decide);
@@ -198,7 +202,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
             const uint32_t bits = (uint32_t)(dead >> gb) & ((1u << W) - 1u);
             if (bits) nk = min(nk, k * W + (int)__builtin_ctz(bits));
         }
-        if (__ballot(close) >> gb & ((1ull << W) - 1ull)) {      // group-uniform, rare: redo with the exact fallback
+        if (close >> gb & ((1ull << W) - 1ull)) {                // group-uniform, rare: redo with the exact fallback
             st = st0;
             nk = E;
             auto decide_exact = [&](auto I) __attribute__((always_inline)) -> bool {
