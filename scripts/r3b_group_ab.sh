@@ -20,16 +20,16 @@ for i in ${ROUNDS:-1 2}; do
     n=$(basename $d)
     run c5x1_${n}_$i $d --config 5 --chains 1 --steps 6 --warmup 2
     run c2x1_${n}_$i $d --config 2 --chains 1 --steps 10 --warmup 2
-    run c5x256_${n}_$i $d --config 5 --steps 3 --warmup 1
+    [ -z "${SKIP_256:-}" ] && run c5x256_${n}_$i $d --config 5 --steps 3 --warmup 1
   done
 done
-for d in ab_old .; do
+[ -z "${SKIP_ABC:-}" ] && for d in ab_old .; do
   n=$(basename $d)
   (cd $ROOT/$d && timeout -k 10 300 python scripts/abc_bench.py ${ABC_ARGS:-}) > $OUT/abc_$n.log 2>&1 || { echo "STOP abc $n"; tail -5 $OUT/abc_$n.log; exit 1; }
   echo "abc_$n $(tail -1 $OUT/abc_$n.log)"
 done
 if [ -n "${SWEEP:-}" ]; then
-  timeout -k 10 400 python scripts/lanes_sweep.py --cfg 2 5 --chains 1 2 8 --lanes 4 8 --reps 3 --out $OUT/lanes_sweep.jsonl > $OUT/sweep.log 2>&1 || { echo "STOP sweep"; tail -5 $OUT/sweep.log; exit 1; }
+  timeout -k 10 400 python scripts/lanes_sweep.py --cfg 2 5 --chains 1 2 8 --lanes ${SWEEP_LANES:-4 8} --reps 3 --out $OUT/lanes_sweep.jsonl > $OUT/sweep.log 2>&1 || { echo "STOP sweep"; tail -5 $OUT/sweep.log; exit 1; }
   cat $OUT/lanes_sweep.jsonl
 fi
 echo done

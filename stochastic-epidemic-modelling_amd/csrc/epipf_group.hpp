@@ -185,6 +185,10 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
             ulo[k] = uc - F::kBand;
             L[k] = neg_log_one_minus_u01<true>(r[k].x, r[k].y, tab);                     // -log(1 - U), :62
         }
+        // sched_barrier(0) fences between the phases (draws | decision pass | extinction + redo | tau | clock): the
+        // scheduler otherwise hoists independent work across the latency-bound passes (measured +1% at config 5,
+        // one chain; profiles/r3d_phase_timing.txt has the per-phase cycles)
+        __builtin_amdgcn_sched_barrier(0);
         const F st0 = st;
         uint64_t close = 0;                              // lanes whose decision did not certify
         auto decide = [&](auto I) __attribute__((always_inline)) -> bool {
@@ -194,6 +198,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
             return true;
         };
         StaticFor<0, E>::run(decide);
+        __builtin_amdgcn_sched_barrier(0);
         // events up to extinction: the first e whose state before it is extinct (the last applied event emptied it)
         int nk = E;
 #pragma unroll
@@ -219,6 +224,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
             for (int k = 0; k < K; ++k)                  // the state before event nk (< E): the extinct one
                 if (k * W + gl == nk) mine[k] = st;
         }
+        __builtin_amdgcn_sched_barrier(0);
         double tau[K];                                   // each event's time, the exact loop's expressions
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -251,7 +257,9 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
             }
             return true;
         };
+        __builtin_amdgcn_sched_barrier(0);
         StaticFor<0, E>::run(clock);
+        __builtin_amdgcn_sched_barrier(0);
         const int stop = inside < nk ? inside : -1;
         t = tt;
         if (stop >= 0 || nk < E) {                       // the step ends before event `end` (past tmax or extinct)
