@@ -1,5 +1,5 @@
-"""Summarise the per-wave phase cycles printed by a phase-timing build of the lane-group step kernel (a local
-diagnostic build with s_memtime brackets around each phase of group_propagate; not shipped).
+"""Summarise the per-wave phase cycles printed by the phase-timing build of the lane-group step kernel (make phase:
+lib/libepipf_phase.so, s_memtime at the phase fences of group_propagate; diagnostic only).
 
     python scripts/r3d_phase_report.py log..."""
 import collections

@@ -131,6 +131,15 @@ __device__ __forceinline__ double exact_scale(const SsaState<MODEL, G>& ex, cons
 //   clock: t + tau in event order, stop at the first t + tau > tmax.
 // Day recorder of the ABC trial (abc_kernels.hip): `days` is every event's clock in order, with the state before it.
 // The filter records nothing.
+// Phase timing (make phase -> lib/libepipf_phase.so, EPIPF_PHASE_TIMING): s_memtime at the phase fences of the chunk
+// loop, summed per lane group; the step kernel prints each sampled wave's totals (scripts/r3d_phase_report.py).
+#ifdef EPIPF_PHASE_TIMING
+#define EPIPF_PHASE_MARK(v)                                  \
+    const unsigned long long v = __builtin_readcyclecounter(); \
+    __builtin_amdgcn_sched_barrier(0)
+#else
+#define EPIPF_PHASE_MARK(v)
+#endif
 struct NoDays {
     static constexpr bool kOn = false;
 };
@@ -138,7 +147,7 @@ struct NoDays {
 template <int MODEL, int G, int W, int K, class Days = NoDays>
 __device__ __forceinline__ int group_propagate(const double* x0, double* xout, const ChainParam& cp, uint32_t j,
                                                uint32_t ptag, double tmax, const LogTab* __restrict__ tab,
-                                               Days* days = nullptr) {
+                                               Days* days = nullptr, unsigned long long* ph = nullptr) {
     using F = typename GroupSsa<MODEL, G>::type;
     constexpr int C = Shape<MODEL, G>::C;
     constexpr int E = W * K;
@@ -175,6 +184,8 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
     }
     F mine[K];                                           // mine[k]: state before event k W + gl
     for (;;) {
+        __builtin_amdgcn_sched_barrier(0);
+        EPIPF_PHASE_MARK(tA);
         Block r[K];
         float ulo[K];
         double L[K];
@@ -189,6 +200,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         // scheduler otherwise hoists independent work across the latency-bound passes (measured +1% at config 5,
         // one chain; profiles/r3d_phase_timing.txt has the per-phase cycles)
         __builtin_amdgcn_sched_barrier(0);
+        EPIPF_PHASE_MARK(tB);
         const F st0 = st;
         uint64_t close = 0;                              // lanes whose decision did not certify
         auto decide = [&](auto I) __attribute__((always_inline)) -> bool {
@@ -199,6 +211,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         };
         StaticFor<0, E>::run(decide);
         __builtin_amdgcn_sched_barrier(0);
+        EPIPF_PHASE_MARK(tC);
         // events up to extinction: the first e whose state before it is extinct (the last applied event emptied it)
         int nk = E;
 #pragma unroll
@@ -225,6 +238,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
                 if (k * W + gl == nk) mine[k] = st;
         }
         __builtin_amdgcn_sched_barrier(0);
+        EPIPF_PHASE_MARK(tD);
         double tau[K];                                   // each event's time, the exact loop's expressions
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -258,8 +272,15 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
             return true;
         };
         __builtin_amdgcn_sched_barrier(0);
+        EPIPF_PHASE_MARK(tE);
         StaticFor<0, E>::run(clock);
         __builtin_amdgcn_sched_barrier(0);
+        EPIPF_PHASE_MARK(tF);
+#ifdef EPIPF_PHASE_TIMING
+        if (ph) {
+            ph[0] += tB - tA; ph[1] += tC - tB; ph[2] += tD - tC; ph[3] += tE - tD; ph[4] += tF - tE; ph[5] += 1;
+        }
+#endif
         const int stop = inside < nk ? inside : -1;
         t = tt;
         if (stop >= 0 || nk < E) {                       // the step ends before event `end` (past tmax or extinct)
@@ -306,6 +327,12 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
     const size_t bcur = ((size_t)cur * a.max_chains + chain) * a.bstride;
     for (int i = (int)threadIdx.x; i < kLogTabEntries; i += 64 * W) tab[i] = a.logtab[i];
 
+#ifdef EPIPF_PHASE_TIMING
+    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
+    const unsigned long long k0 = __builtin_readcyclecounter();
+#else
+    unsigned long long* ph = nullptr;
+#endif
     if (wave == 0) {                                     // likelihood, resampling, gather: pf_step_kernel's code
         const int j = bp.b * 64 + lane;
         const double total = (a.seg == 1)
@@ -355,6 +382,9 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
         }
     }
     __syncthreads();
+#ifdef EPIPF_PHASE_TIMING
+    const unsigned long long k1 = __builtin_readcyclecounter();
+#endif
     if (!(red[0] > 0.0)) return;                         // block-uniform
 
     // group SSA: wave w, group g runs particle w * PPW + g of the block
@@ -368,8 +398,11 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
 #pragma unroll
         for (int c = 0; c < C; ++c) x0[c] = (double)rows[pl * C + c];
         const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
-        nev = group_propagate<MODEL, G, W, K>(x0, x, cp, (uint32_t)jg, ptag, 1.0, tab);
+        nev = group_propagate<MODEL, G, W, K>(x0, x, cp, (uint32_t)jg, ptag, 1.0, tab, (NoDays*)nullptr, ph);
     }
+#ifdef EPIPF_PHASE_TIMING
+    const unsigned long long k2 = __builtin_readcyclecounter();
+#endif
     __syncthreads();                                     // every group has read its parent row
     if (jg < a.N && gl == 0) {
 #pragma unroll
@@ -402,6 +435,12 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
             if (lane == 63) a.bsum[bcur + bp.b] = loc;
         }
     }
+#ifdef EPIPF_PHASE_TIMING
+    if (lane == 0 && bp.b % 16 == 0 && (a.T < 50 || p % 20 == 0))
+        printf("PH p=%d b=%d w=%d ch=%llu pre=%llu ssa=%llu bar=0 post=%llu draws=%llu decide=%llu ball=%llu tau=%llu "
+               "clock=%llu nev=%d\n", p, bp.b, wave, ph[5], k1 - k0, k2 - k1, __builtin_readcyclecounter() - k2, ph[0],
+               ph[1], ph[2], ph[3], ph[4], nev);
+#endif
 }
 
 // ------------------------------------------------------------------------------- launch table
