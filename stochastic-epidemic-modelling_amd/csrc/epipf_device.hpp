@@ -594,6 +594,32 @@ struct FastSubgroups {                                                 // gilles
             I[r] += hit ? dI : 0.f;
         }
     }
+    // the event from the wave masks below[i] of the certified sides c_i < U total (channel ch fired iff below[ch - 1]
+    // and not below[ch]; FastSubgroupsPacked::apply_below), keeping the per-group changes for an undo
+    __device__ __forceinline__ void apply_below(const uint64_t* below, float* dS, float* dI) {
+        auto hit = [&](int ch) __attribute__((always_inline)) -> uint64_t {
+            return (ch == 0 ? ~0ull : below[ch - 1]) & (ch == NCH - 1 ? ~0ull : ~below[ch]);
+        };
+#pragma unroll
+        for (int r = 0; r < G; ++r) {
+            uint64_t inf = 0;
+#pragma unroll
+            for (int g = 0; g < G; ++g) inf |= hit(g * (G + 1) + r);
+            const bool fi = __builtin_amdgcn_inverse_ballot_w64(inf);
+            const bool fr = __builtin_amdgcn_inverse_ballot_w64(hit(r * (G + 1) + G));
+            dS[r] = fi ? 1.f : 0.f;
+            dI[r] = fi ? 1.f : (fr ? -1.f : 0.f);
+            S[r] = S[r] - dS[r];
+            I[r] = I[r] + dI[r];
+        }
+    }
+    __device__ __forceinline__ void undo(const float* dS, const float* dI) {
+#pragma unroll
+        for (int r = 0; r < G; ++r) {
+            S[r] = S[r] + dS[r];
+            I[r] = I[r] - dI[r];
+        }
+    }
     __device__ __forceinline__ int save(double* x) const {
         float inf = S0sum, rec = -R0sum;
 #pragma unroll
@@ -789,6 +815,8 @@ __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, 
     uint32_t ks = 0;                                                   // event index, wave-uniform (SGPR)
     bool alive = st.active(), ok = true;
     int ch = 0;
+    constexpr int GD = NCH > 3 ? G : 1;
+    float dS[GD], dI[GD];                                              // the last event's changes (subgroups)
     Block rn{0u, 0u, 0u, 0u};
     if (alive) rn = philox<true>(0u, j, ptag, cp.f, cp.k0, cp.k1);    // x word inverted: ~x
     while (alive) {
@@ -799,24 +827,36 @@ __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, 
         const float total = st.cum(c);
         const float ri = __builtin_amdgcn_rcpf(total);
         const float uc = __uint_as_float(0x3F800000u | (r.w >> 9)) - (1.0f - kUlpF);   // uf + 2^-24
-        bool close = false;
-        ch = 0;
+        uint64_t below[NCH - 1];
         if constexpr (NCH <= 3) {                                      // ratios q_i = c_i / total
+            bool close = false;
+            ch = 0;
 #pragma unroll
             for (int i = 0; i < NCH - 1; ++i) {                        // numpy choice, searchsorted right
                 const float q = c[i] * ri;
                 ch += (q < uc) ? 1 : 0;
                 close |= fabsf(q - uc) <= F::kBand;
             }
-        } else {                                                       // c_i against uc * total: one multiply
-            const float T = uc * total, band = F::kBand * total;       // per draw instead of one per channel
+            if (close) ch = st.exact_channel(cp, u01(r.z, r.w));
+        } else {
+            // c_i against U total as wave masks, the lane-group pass's certified bracket (decide_flagged,
+            // epipf_group.hpp: Tlo = fl((uc - kBand) total), Thi = fl(Tlo + 2 kBand total)); a lane with some c_i in
+            // between takes the reference expression in f64 and its bits of the masks are replaced
+            const float Tlo = (uc - F::kBand) * total, Thi = fmaf(2.0f * F::kBand, total, Tlo);
+            uint64_t unsure = 0;
 #pragma unroll
             for (int i = 0; i < NCH - 1; ++i) {
-                ch += (c[i] < T) ? 1 : 0;
-                close |= fabsf(c[i] - T) <= band;
+                below[i] = __ballot(c[i] < Tlo);
+                unsure |= below[i] ^ __ballot(c[i] < Thi);
+            }
+            if (unsure) {                                              // wave-uniform, rare
+                const bool mine = __builtin_amdgcn_inverse_ballot_w64(unsure);
+                int che = 0;
+                if (mine) che = st.exact_channel(cp, u01(r.z, r.w));
+#pragma unroll
+                for (int i = 0; i < NCH - 1; ++i) below[i] = (below[i] & ~unsure) | __ballot(mine && che > i);
             }
         }
-        if (close) ch = st.exact_channel(cp, u01(r.z, r.w));
         const uint32_t nh = ~r.y;
         float lg = __builtin_amdgcn_logf((float)nh * 0x1.0p-32f);     // 1 - U from its top word: <= 2 ulp for x >= 2^-8
         if (nh < 0x1000000u) {                                         // 1 - U < 2^-8: 0.4% of events
@@ -828,12 +868,14 @@ __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, 
         df = (float)rem;
         B = fmaf(R, kClockRF, Bt);
         ok = df > B;                                                   // certainly inside the step
-        st.apply(ch, 1.f);                                             // undone below if the lane overshoots
+        if constexpr (NCH <= 3) st.apply(ch, 1.f);                     // undone below if the lane overshoots
+        else st.apply_below(below, dS, dI);
         alive = ok && st.active();
     }
     if (!ok) {
         if (!(df < -B)) return false;                                 // boundary too close to call: exact loop
-        st.apply(ch, -1.f);                                            // the overshooting event is not applied
+        if constexpr (NCH <= 3) st.apply(ch, -1.f);                    // the overshooting event is not applied
+        else st.undo(dS, dI);
     }
     nev_out = st.save(x);
     iters = nev_out + (ok ? 0 : 1);
