@@ -454,8 +454,14 @@ struct FastSsa<kSIR, 1> {                                              // gilles
         S = S - (ch == 0 ? s : 0.f);
         I = I + (ch == 0 ? s : -s);
     }
+    // the counts of s where c holds (the lane-group pass keeps each lane's state before its event with selects, one
+    // basic block for the whole pass; the other fields are the particle-step's constants)
+    __device__ __forceinline__ void keep_if(bool c, const FastSsa& s) {
+        S = c ? s.S : S;
+        I = c ? s.I : I;
+    }
     // the event from the wave masks below[i] of the certified sides c_i < U total (the lane-group pass,
-    // epipf_group.hpp: decide_flagged); the selects take the masks as their SGPR conditions
+    // epipf_group.hpp: decide_lo); the selects take the masks as their SGPR conditions
     __device__ __forceinline__ void apply_below(const uint64_t* below) {
         const bool rec = __builtin_amdgcn_inverse_ballot_w64(below[0]);
         S = S - (rec ? 0.f : 1.f);
@@ -499,6 +505,11 @@ struct FastSsa<kSEIR, 1> {                                             // gilles
         S = S - (ch == 0 ? s : 0.f);
         E = E + (ch == 0 ? s : (ch == 1 ? -s : 0.f));
         I = I + (ch == 1 ? s : (ch == 2 ? -s : 0.f));
+    }
+    __device__ __forceinline__ void keep_if(bool c, const FastSsa& s) {
+        S = c ? s.S : S;
+        E = c ? s.E : E;
+        I = c ? s.I : I;
     }
     __device__ __forceinline__ void apply_below(const uint64_t* below) {   // below[1] implies below[0]
         const bool b0 = __builtin_amdgcn_inverse_ballot_w64(below[0]), b1 = __builtin_amdgcn_inverse_ballot_w64(below[1]);
@@ -654,6 +665,13 @@ struct FastSubgroupsPacked {                                           // gilles
         f2 r;
         asm("v_pk_mul_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
         return r;
+    }
+    __device__ __forceinline__ void keep_if(bool c, const FastSubgroupsPacked& s) {
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            S2[p] = c ? s.S2[p] : S2[p];
+            I2[p] = c ? s.I2[p] : I2[p];
+        }
     }
     __device__ __forceinline__ float S(int q) const { return S2[q >> 1][q & 1]; }
     __device__ __forceinline__ float I(int q) const { return I2[q >> 1][q & 1]; }
@@ -839,7 +857,7 @@ __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, 
             }
             if (close) ch = st.exact_channel(cp, u01(r.z, r.w));
         } else {
-            // c_i against U total as wave masks, the lane-group pass's certified bracket (decide_flagged,
+            // c_i against U total as wave masks, the lane-group pass's certified bracket (decide_lo,
             // epipf_group.hpp: Tlo = fl((uc - kBand) total), Thi = fl(Tlo + 2 kBand total)); a lane with some c_i in
             // between takes the reference expression in f64 and its bits of the masks are replaced
             const float Tlo = (uc - F::kBand) * total, Thi = fmaf(2.0f * F::kBand, total, Tlo);

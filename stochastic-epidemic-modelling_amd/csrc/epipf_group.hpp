@@ -81,25 +81,33 @@ __device__ __forceinline__ double group_lane_f64(double v) {
 // brackets U total: with ulo = uc - kBand (exact: uc is an odd multiple of 2^-24 below 1 and kBand a power of two
 // >= 2^-19), Tlo = fl(ulo total) and Thi = fl(Tlo + 2 kBand total), c_i < Tlo puts channel i's cumulative rate
 // certainly below U total and c_i >= Thi certainly above: the product form's band (FastSsa) less one
-// ulp of total for the two roundings, inside kBand's margin over 2 e_as + 2 ulp.  A lane of a live particle with
-// some c_i in between raises its bit of `close` (the caller then redoes the chunk on the exact fallback).  The
-// comparisons are taken as wave masks: the decision, its certificate and `close` are SALU logic, and the state
-// update is two or three selects per count on those masks (FastSsa::apply_below).  No branch: the lane-group pass
-// runs this once per event on its critical path.
+// ulp of total for the two roundings, inside kBand's margin over 2 e_as + 2 ulp.  The pass decides on the Tlo side
+// alone (decide_lo: the comparisons as wave masks, the channel as SALU logic on them, the state update as selects on
+// the masks, FastSsa::apply_below); whether every c_i also lies on the same side of Thi is checked after the pass,
+// by the lane that drew the event, on the state before it (event_certified: the same arithmetic on the same values,
+// in the parallel phase instead of on the pass's dependent chain).  A live particle's uncertified event makes the
+// caller redo the chunk on the exact fallback.
 template <typename F>
-__device__ __forceinline__ void decide_flagged(F& st, float ulo, uint64_t& close) {
+__device__ __forceinline__ void decide_lo(F& st, float ulo) {
     constexpr int NCH = F::NCH;
     float c[NCH - 1];
-    const float total = st.cum(c);
-    const float Tlo = ulo * total, Thi = fmaf(2.0f * F::kBand, total, Tlo);
-    uint64_t below[NCH - 1], unsure = 0;
+    const float Tlo = ulo * st.cum(c);
+    uint64_t below[NCH - 1];
 #pragma unroll
-    for (int i = 0; i < NCH - 1; ++i) {
-        below[i] = __ballot(c[i] < Tlo);
-        unsure |= below[i] ^ __ballot(c[i] < Thi);
-    }
-    close |= unsure & __ballot(st.active());
+    for (int i = 0; i < NCH - 1; ++i) below[i] = __ballot(c[i] < Tlo);
     st.apply_below(below);
+}
+
+template <typename F>
+__device__ __forceinline__ bool event_certified(const F& s, float ulo) {
+    constexpr int NCH = F::NCH;
+    float c[NCH - 1];
+    const float total = s.cum(c);
+    const float Tlo = ulo * total, Thi = fmaf(2.0f * F::kBand, total, Tlo);
+    bool sure = true;
+#pragma unroll
+    for (int i = 0; i < NCH - 1; ++i) sure = sure && ((c[i] < Tlo) == (c[i] < Thi));
+    return sure || !s.active();
 }
 
 // 1/sum(a) of the exact state (the reference's expressions, SsaState::rates)
@@ -123,7 +131,8 @@ __device__ __forceinline__ double exact_scale(const SsaState<MODEL, G>& ex, cons
 //
 // Chunk of E = W K events, event e drawn by lane e % W in its slot e / W:
 //   per lane, independent of the state: K Philox blocks, their channel uniforms uc and -log(1 - U) (glibc's log);
-//   pass: E channel decisions in order, branch-free (decide_flagged); lane e % W keeps the state before event e;
+//   pass: E channel decisions in order, branch-free (decide_lo); lane e % W keeps the state before event e and
+//          then checks that event's certificate (event_certified);
 //   after: the first event whose state is extinct (ballots) -> events in the chunk; if any decision was not
 //          certified, the pass is redone with the exact fallback per event;
 //   per lane: each kept state's 1/sum(a) (two IEEE divisions) times its -log(1 - U) = tau (SsaState::tau_of's
@@ -183,6 +192,8 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         return 0;
     }
     F mine[K];                                           // mine[k]: state before event k W + gl
+#pragma unroll
+    for (int k = 0; k < K; ++k) mine[k] = st;            // the particle-step's constants; the counts kept per event
     for (;;) {
         __builtin_amdgcn_sched_barrier(0);
         EPIPF_PHASE_MARK(tA);
@@ -202,14 +213,16 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         __builtin_amdgcn_sched_barrier(0);
         EPIPF_PHASE_MARK(tB);
         const F st0 = st;
-        uint64_t close = 0;                              // lanes whose decision did not certify
         auto decide = [&](auto I) __attribute__((always_inline)) -> bool {
             constexpr int e = decltype(I)::value;
-            if (gl == e % W) mine[e / W] = st;
-            decide_flagged(st, __uint_as_float(group_lane_dpp<W, e % W>(__float_as_uint(ulo[e / W]))), close);
+            mine[e / W].keep_if(gl == e % W, st);
+            decide_lo(st, __uint_as_float(group_lane_dpp<W, e % W>(__float_as_uint(ulo[e / W]))));
             return true;
         };
         StaticFor<0, E>::run(decide);
+        bool uncertified = false;                        // this lane's events, on the states before them
+#pragma unroll
+        for (int k = 0; k < K; ++k) uncertified = uncertified || !event_certified(mine[k], ulo[k]);
         __builtin_amdgcn_sched_barrier(0);
         EPIPF_PHASE_MARK(tC);
         // events up to extinction: the first e whose state before it is extinct (the last applied event emptied it)
@@ -220,7 +233,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
             const uint32_t bits = (uint32_t)(dead >> gb) & ((1u << W) - 1u);
             if (bits) nk = min(nk, k * W + (int)__builtin_ctz(bits));
         }
-        if (close >> gb & ((1ull << W) - 1ull)) {                // group-uniform, rare: redo with the exact fallback
+        if (__ballot(uncertified) >> gb & ((1ull << W) - 1ull)) {   // group-uniform, rare: redo with the exact fallback
             st = st0;
             nk = E;
             auto decide_exact = [&](auto I) __attribute__((always_inline)) -> bool {
