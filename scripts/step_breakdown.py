@@ -14,7 +14,7 @@ from epipf import pmcmc as pm  # noqa: E402
 
 Y, meta = datasets.benchmark_dataset(int(os.environ.get("CFG", 2)))
 C = int(os.environ.get("CHAINS", 256))
-s = pm.ChainSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=12, probs=meta["probs"],
+s = pm.ChainSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=int(os.environ.get("K", 6)) + 4, probs=meta["probs"],
                     observations=meta.get("observations", False), n_particles=meta["N"],
                     n_population=meta["n_population"], mu=meta["mu"],
                     rngs=[np.random.RandomState(2024 + g) for g in range(C)],
@@ -43,7 +43,7 @@ s.step()
 s.eng.reset_stats()
 s.eng.set_profiling(_lib.PROFILE_TIMING)
 tim = {"run": 0.0, "path": 0.0}
-K = 6
+K = int(os.environ.get("K", 6))
 t0 = time.perf_counter()
 for _ in range(K):
     s.step()

@@ -37,15 +37,17 @@
 
 namespace epipf {
 
-// Value of lane I of this lane's group of W consecutive lanes: DPP moves (groups of W <= 16 lie inside one DPP row).
+// Value of lane I of this lane's group of W consecutive lanes: DPP moves (groups of W <= 16 lie inside one DPP row),
+// a swizzle for W = 8.
 template <int W, int I>
 __device__ __forceinline__ uint32_t group_lane_dpp(uint32_t v) {
     static_assert(I >= 0 && I < W, "lane inside the group");
     if constexpr (W == 16) {
         return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + I, 0xF, 0xF, false);       // row_newbcast:I
-    } else if constexpr (W == 8) {                                      // two groups per row: one bank pair each
-        const int lo = __builtin_amdgcn_update_dpp(0, (int)v, 0x150 + I, 0xF, 0x3, false);
-        return (uint32_t)__builtin_amdgcn_update_dpp(lo, (int)v, 0x150 + 8 + I, 0xF, 0xC, false);
+    } else if constexpr (W == 8) {
+        // two groups per DPP row would take two bank-masked row_newbcast moves and a zeroing move; one ds_swizzle in
+        // bitmask mode (source lane (lane & 0x18) | I within each half-wave) goes through the LDS crossbar instead
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (I << 5));
     } else if constexpr (W == 4) {
         return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, I | (I << 2) | (I << 4) | (I << 6), 0xF, 0xF, false);
     } else {
