@@ -112,13 +112,13 @@ struct epipf_ctx {
 // Lanes per particle for a run of n_chains filters.  The one-lane kernel needs ~20k waves per launch to fill the
 // chip; below 8 chains of 10^4 particles (n_chains x B <= 1280 particle blocks) the lane-group kernel with W = 4
 // runs each particle-step 1.6-2.1x faster (1-8 chains, BASELINE configs 2 and 5: profiles/r2e_lanes_sweep*.jsonl;
-// W = 2, 16 and K > 1 measured no better).  Up to 160 blocks (one chain of 10^4) W = 8 is faster since the
-// mask-based decision pass (round 3: configs 2 / 3 / 5 +2% / +10% / +1%, profiles/r3c_lanes_sweep.jsonl); from two
-// chains on, W = 4.
+// W = 2, 16 and K > 1 measured no better).  Up to 640 blocks (4 chains of 10^4) W = 8 is faster since round 3's
+// mask-based decision pass and swizzle broadcasts (one chain: configs 2 / 3 / 5 +10% / +8% / +9%, four chains
+// +3% / 0% / +9%; at 8 chains W = 4 leads by 16-29%: profiles/r3k_lanes_sweep_chains.jsonl).
 static int pick_lanes(const epipf_ctx* c, int n_chains) {
     if (c->lanes > 0) return c->lanes;
     const long blocks = (long)n_chains * c->B;
-    return blocks <= 160 ? 8 : blocks <= (long)c->lane_blocks ? 4 : 1;
+    return blocks <= (long)c->lane_blocks / 2 ? 8 : blocks <= (long)c->lane_blocks ? 4 : 1;
 }
 
 static int pick_lane_events(const epipf_ctx* c, int W) {
