@@ -173,6 +173,7 @@ __global__ __launch_bounds__(256) void abc_trials_group_kernel(AbcArgs a) {
         cp.f = a.f; cp.k0 = a.k0; cp.k1 = a.k1;
         cp.flags = kChainFastSsa;
         cp.clock_slack = 1.f;
+        cp.band_slack = 1.f;
         AbcDays d{a.days + i, n, 0, 0.0, gl == 0, &a};
         double xf[3];
         nev = group_propagate<kSIR, 1, W, 1, AbcDays>(x, xf, cp, t, kDomainAbcSsa, a.last_day, tab, &d);

@@ -93,6 +93,8 @@ struct epipf_ctx {
     double abc_group_frac = 0.5, abc_frac = 0.5;   // share of the sorted trials on lane groups (EPIPF_ABC_GROUP_FRAC)
     bool fast_ssa = true;    // certified f32 event loop (EPIPF_SSA_FAST=0 disables; results are identical)
     float clock_slack = 1.f; // EPIPF_CLOCK_SLACK >= 1 widens its clock band: replays on purpose (stress tests)
+    float band_slack = 1.f;  // EPIPF_BAND_SLACK >= 1 widens the channel decision's band: exact decisions and redone
+                             // lane-group chunks on purpose (stress tests)
     double tie_scale = 1.0;  // EPIPF_TIE_SCALE >= 1 widens particle_weight's tie band: the all-columns pass on purpose
     int n_streams = 4;   // chain groups on concurrent streams (EPIPF_STREAMS overrides, 1..kMaxFilterStreams)
     hipStream_t aux[kMaxFilterStreams] = {};
@@ -226,6 +228,7 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     c->wg = default_wg(n_particles);
     if (const char* e = getenv("EPIPF_SSA_FAST")) c->fast_ssa = atoi(e) != 0;
     if (const char* e = getenv("EPIPF_CLOCK_SLACK")) c->clock_slack = std::max(1.0f, std::min(1e6f, (float)atof(e)));
+    if (const char* e = getenv("EPIPF_BAND_SLACK")) c->band_slack = std::max(1.0f, std::min(1e4f, (float)atof(e)));
     if (const char* e = getenv("EPIPF_TIE_SCALE")) c->tie_scale = std::max(1.0, std::min(1e300, atof(e)));
     if (const char* e = getenv("EPIPF_STREAMS")) c->n_streams = std::max(1, std::min(kMaxFilterStreams, atoi(e)));
     if (const char* e = getenv("EPIPF_LANES")) {
@@ -377,6 +380,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
         q.f = filter_index[ch];
         q.flags = c->fast_ssa ? kChainFastSsa : 0u;
         q.clock_slack = c->clock_slack;
+        q.band_slack = c->band_slack;
         c->h_status[ch] = on ? EPIPF_STATUS_OK : EPIPF_STATUS_SKIPPED;
         n_active += on;
     }
@@ -565,6 +569,7 @@ int epipf_simulate(epipf_ctx* c, int n, const int32_t* states_in, const double* 
     q.k0 = (uint32_t)key; q.k1 = (uint32_t)(key >> 32); q.f = filter_index;
     q.flags = c->fast_ssa ? kChainFastSsa : 0u;
     q.clock_slack = c->clock_slack;
+    q.band_slack = c->band_slack;
     HIP_TRY(hipMemcpyAsync(dcp, &q, sizeof q, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(din, states_in, sizeof(int32_t) * (size_t)n * c->C, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(dev_events, 0, sizeof(unsigned long long), c->stream));
@@ -612,6 +617,8 @@ int epipf_simulate_path(epipf_ctx* c, int n, const int32_t* states_in, const dou
     memset(&q, 0, sizeof q);
     for (int i = 0; i < d; ++i) { q.theta[i] = theta[i]; q.thetaf[i] = (float)theta[i]; }
     q.k0 = (uint32_t)key; q.k1 = (uint32_t)(key >> 32); q.f = filter_index;
+    q.clock_slack = 1.f;
+    q.band_slack = 1.f;
     HIP_TRY(hipMemcpyAsync(dcp, &q, sizeof q, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(din, states_in, sizeof(int32_t) * (size_t)n * C, hipMemcpyHostToDevice, c->stream));
     SimPathArgs a{};

@@ -95,6 +95,8 @@ struct ChainParam {
     uint32_t flags;            // kChainFastSsa: the certified f32 event loop may run (EPIPF_SSA_FAST=0 clears it)
     float thetaf[kMaxTheta];   // theta rounded to f32 on the host (scalar loads: the fast path's rates stay in SGPRs)
     float clock_slack;         // >= 1: widens the f32 loop's clock band (more replays, same results); tests only
+    float band_slack;          // >= 1: widens the channel decision's band (more exact decisions and redone chunks,
+                               // same results); tests only
 };
 constexpr uint32_t kChainFastSsa = 1u;   // (all models)
 
@@ -827,6 +829,7 @@ __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, 
     F st;
     if (!st.load(x, cp)) return false;
     eligible = true;
+    const float kB = F::kBand * cp.band_slack;                         // the decision band (slack 1: kBand)
     double rem = tmax * kInvLn2;                                       // remaining time, units of 1/ln 2
     const float Bt = (float)rem * F::kClockT * cp.clock_slack;
     float R = 0.f, df = 0.f, B = 0.f;
@@ -853,14 +856,14 @@ __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, 
             for (int i = 0; i < NCH - 1; ++i) {                        // numpy choice, searchsorted right
                 const float q = c[i] * ri;
                 ch += (q < uc) ? 1 : 0;
-                close |= fabsf(q - uc) <= F::kBand;
+                close |= fabsf(q - uc) <= kB;
             }
             if (close) ch = st.exact_channel(cp, u01(r.z, r.w));
         } else {
             // c_i against U total as wave masks, the lane-group pass's certified bracket (decide_lo,
             // epipf_group.hpp: Tlo = fl((uc - kBand) total), Thi = fl(Tlo + 2 kBand total)); a lane with some c_i in
             // between takes the reference expression in f64 and its bits of the masks are replaced
-            const float Tlo = (uc - F::kBand) * total, Thi = fmaf(2.0f * F::kBand, total, Tlo);
+            const float Tlo = (uc - kB) * total, Thi = fmaf(2.0f * kB, total, Tlo);
             uint64_t unsure = 0;
 #pragma unroll
             for (int i = 0; i < NCH - 1; ++i) {
@@ -953,10 +956,10 @@ __device__ __forceinline__ int fast_channel(const F& st, const ChainParam& cp, u
         for (int i = 0; i < NCH - 1; ++i) {
             const float q = c[i] * ri;
             ch += (q < uc) ? 1 : 0;
-            close |= fabsf(q - uc) <= F::kBand;
+            close |= fabsf(q - uc) <= F::kBand * cp.band_slack;
         }
     } else {
-        const float T = uc * total, band = F::kBand * total;
+        const float T = uc * total, band = F::kBand * cp.band_slack * total;
 #pragma unroll
         for (int i = 0; i < NCH - 1; ++i) {
             ch += (c[i] < T) ? 1 : 0;

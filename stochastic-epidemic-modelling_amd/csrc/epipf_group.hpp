@@ -88,7 +88,8 @@ __device__ __forceinline__ double group_lane_f64(double v) {
 // the masks, FastSsa::apply_below); whether every c_i also lies on the same side of Thi is checked after the pass,
 // by the lane that drew the event, on the state before it (event_certified: the same arithmetic on the same values,
 // in the parallel phase instead of on the pass's dependent chain).  A live particle's uncertified event makes the
-// caller redo the chunk on the exact fallback.
+// caller redo the chunk on the exact fallback.  (A test's band_slack > 1 scales kBand: a wider bracket only moves more
+// events to the exact fallback.)
 template <typename F>
 __device__ __forceinline__ void decide_lo(F& st, float ulo) {
     constexpr int NCH = F::NCH;
@@ -101,11 +102,11 @@ __device__ __forceinline__ void decide_lo(F& st, float ulo) {
 }
 
 template <typename F>
-__device__ __forceinline__ bool event_certified(const F& s, float ulo) {
+__device__ __forceinline__ bool event_certified(const F& s, float ulo, float kB) {
     constexpr int NCH = F::NCH;
     float c[NCH - 1];
     const float total = s.cum(c);
-    const float Tlo = ulo * total, Thi = fmaf(2.0f * F::kBand, total, Tlo);
+    const float Tlo = ulo * total, Thi = fmaf(2.0f * kB, total, Tlo);
     bool sure = true;
 #pragma unroll
     for (int i = 0; i < NCH - 1; ++i) sure = sure && ((c[i] < Tlo) == (c[i] < Thi));
@@ -193,6 +194,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         put(st, 0);
         return 0;
     }
+    const float kB = F::kBand * cp.band_slack;           // the decision band (slack 1: kBand, exact in ulo)
     F mine[K];                                           // mine[k]: state before event k W + gl
 #pragma unroll
     for (int k = 0; k < K; ++k) mine[k] = st;            // the particle-step's constants; the counts kept per event
@@ -206,7 +208,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         for (int k = 0; k < K; ++k) {
             r[k] = philox(base + (uint32_t)(k * W + gl), j, ptag, cp.f, cp.k0, cp.k1);
             const float uc = __uint_as_float(0x3F800000u | (r[k].w >> 9)) - (1.0f - kUlpF);   // uf + 2^-24
-            ulo[k] = uc - F::kBand;
+            ulo[k] = uc - kB;
             L[k] = neg_log_one_minus_u01<true>(r[k].x, r[k].y, tab);                     // -log(1 - U), :62
         }
         // sched_barrier(0) fences between the phases (draws | decision pass | extinction + redo | tau | clock): the
@@ -224,7 +226,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         StaticFor<0, E>::run(decide);
         bool uncertified = false;                        // this lane's events, on the states before them
 #pragma unroll
-        for (int k = 0; k < K; ++k) uncertified = uncertified || !event_certified(mine[k], ulo[k]);
+        for (int k = 0; k < K; ++k) uncertified = uncertified || !event_certified(mine[k], ulo[k], kB);
         __builtin_amdgcn_sched_barrier(0);
         EPIPF_PHASE_MARK(tC);
         // events up to extinction: the first e whose state before it is extinct (the last applied event emptied it)

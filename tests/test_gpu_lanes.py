@@ -63,6 +63,29 @@ def test_lane_groups_match_oracle(datasets_golden, model, lanes):
         np.testing.assert_allclose(lz[ch], o["log_zetas"], rtol=1e-12, atol=1e-9)
 
 
+@pytest.mark.parametrize("lanes", [1, 4, 8])
+@pytest.mark.parametrize("model", ["sir", "sir_normal", "seir", "sir_subgroups", "sir_subgroups2"])
+def test_widened_decision_band_equals_oracle(datasets_golden, monkeypatch, model, lanes):
+    """Stress the uncertified-decision paths: the channel decision's band widened 3000x (EPIPF_BAND_SLACK, read at
+    create) sends ~1% of decisions to the exact fallback -- the lane groups redo ~8% of their chunks after their
+    per-lane certificates fail, the one-lane loop replaces the unsure lanes' mask bits (subgroups) or takes the
+    f64 channel (SIR, SEIR) -- and states, ancestors and likelihoods stay the oracle's."""
+    monkeypatch.setenv("EPIPF_BAND_SLACK", "3000")
+    c = _case(datasets_golden, model)
+    name = c.get("model", model)
+    N, chains = 700, 2
+    keys, fidx = [41, 42], [5, 11]
+    lz, st, hid, anc, used = _run(name, c, N, chains, lanes, keys, fidx)
+    assert used == lanes
+    for ch in range(chains):
+        o = oracle.particle_filter(c["Y"], name, c["theta"], c["obs"], c["probs"], N, c["npop"], c["mu"],
+                                   key=keys[ch], filter_index=fidx[ch])
+        assert int(st[ch]) == o["status"] == 0
+        np.testing.assert_array_equal(hid[ch], o["hidden"])
+        np.testing.assert_array_equal(anc[ch], o["ancestry"])
+        np.testing.assert_allclose(lz[ch], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("model", ["sir", "seir", "sir_subgroups"])
 def test_every_lane_shape_matches_oracle(datasets_golden, model, shape):
