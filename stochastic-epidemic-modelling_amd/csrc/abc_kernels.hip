@@ -44,9 +44,13 @@ __device__ __forceinline__ void abc_trial_start(const AbcArgs& a, uint32_t t, Ch
 // day row as the clock passes it: day d holds the state after every event with time <= d.  `write`: this lane
 // stores the rows (the lane-group kernel runs it on every lane of a group, one of which writes).  Returns the events;
 // x holds the final state, day the first row not yet written, iters the loop iterations.
+// Early rejection: `acc` sums |I_d - Y_I,d| + |R_d - Y_R,d| over the rows passed (the distance's terms,
+// abc_algo.py:12); once it exceeds `reject_sum` the distance of the full table is provably above the threshold
+// (epipf_abc's bound) and the walk stops with `rejected` set -- the rest of the path cannot change the
+// trial's fate, and a rejected trial's table is never read.  reject_sum = INFINITY: never.
 __device__ __forceinline__ int abc_exact_path(double* x, const ChainParam& cp, uint32_t t, const AbcArgs& a,
                                               const LogTab* __restrict__ tab, int32_t* col, bool write, int& day,
-                                              double& next_day, int& iters) {
+                                              double& next_day, int& iters, double reject_sum, bool& rejected) {
     const size_t n = (size_t)a.n;
     SsaState<kSIR, 1> st;
     st.load(x, cp);
@@ -56,6 +60,8 @@ __device__ __forceinline__ int abc_exact_path(double* x, const ChainParam& cp, u
     uint32_t k = 0;
     int nev = 0;
     bool alive = st.active();
+    double acc = 0.0;
+    rejected = false;
     Block rn{0u, 0u, 0u, 0u};
     if (alive) rn = philox(0u, t, kDomainAbcSsa, a.f, a.k0, a.k1);
     while (alive) {                          // every lane enters at k = 0: k stays wave-uniform
@@ -68,19 +74,22 @@ __device__ __forceinline__ int abc_exact_path(double* x, const ChainParam& cp, u
         if (ev) {
             ++nev;
             while (next_day < clock) {                                   // days the event does not reach
-                if (write) write_day(col, n, day, S0, I0, R0 + (double)rec0);
+                const double R = R0 + (double)rec0;
+                if (write) write_day(col, n, day, S0, I0, R);
+                acc += fabs(I0 - a.Y[3 * day + 1]) + fabs(R - a.Y[3 * day + 2]);
                 ++day;
                 next_day += 1.0;
             }
+            rejected = acc > reject_sum;
         }
-        alive = ev && st.active();
+        alive = ev && st.active() && !rejected;
     }
     st.save(x);
     iters = (int)k;
     return nev;
 }
 
-__global__ __launch_bounds__(256) void abc_trials_kernel(AbcArgs a) {
+__global__ __launch_bounds__(256, 8) void abc_trials_kernel(AbcArgs a) {   // 8 waves per SIMD: <= 64 VGPRs
     __shared__ LogTab tab[kLogTabEntries];
     if (threadIdx.x < kLogTabEntries) tab[threadIdx.x] = a.logtab[threadIdx.x];
     __syncthreads();
@@ -96,8 +105,10 @@ __global__ __launch_bounds__(256) void abc_trials_kernel(AbcArgs a) {
         int32_t* col = a.days + i;
         int day = 0;
         double next_day = 0.0;
-        nev = abc_exact_path(x, cp, t, a, tab, col, true, day, next_day, iters);
-        for (; day < a.T; ++day) write_day(col, n, day, x[0], x[1], x[2]);
+        bool rejected;
+        nev = abc_exact_path(x, cp, t, a, tab, col, true, day, next_day, iters, a.reject_sum, rejected);
+        if (rejected) col[0] = -1;                                   // row 0's S: abc_distance_kernel's marker
+        else for (; day < a.T; ++day) write_day(col, n, day, x[0], x[1], x[2]);
         a.theta[i] = cp.theta[0];
         a.theta[n + i] = cp.theta[1];
     }
@@ -149,7 +160,8 @@ struct AbcDays {
     __device__ __forceinline__ int exact(double* x, const ChainParam& cp, uint32_t t, uint32_t, double,
                                          const LogTab* __restrict__ tab) {
         int iters = 0;
-        return abc_exact_path(x, cp, t, *a, tab, col, lead, day, next_day, iters);
+        bool rejected;
+        return abc_exact_path(x, cp, t, *a, tab, col, lead, day, next_day, iters, INFINITY, rejected);
     }
 };
 
@@ -234,6 +246,10 @@ __global__ __launch_bounds__(256) void abc_distance_kernel(AbcArgs a) {
     if (i >= a.n) return;
     const size_t n = (size_t)a.n;
     const int32_t* col = a.days + i;
+    if (col[0] < 0) {                                              // rejected early by abc_trials_kernel
+        a.dist[i] = INFINITY;
+        return;
+    }
     const AbsDiff vi{col + n, 3 * n, a.Y + 1}, vr{col + 2 * n, 3 * n, a.Y + 2};
     const double dT = (double)a.T;
     const double si = DEEP ? pairwise_sum<kAbcPairwiseDepth>(vi, 0, a.T) : pairwise_leaf(vi, 0, a.T);

@@ -729,6 +729,7 @@ int abc_prepare(epipf_ctx* c, const double* Y, int T, const double* priors, uint
         a.pm[q] = lam > 0.0 ? std::exp(-lam + lam * std::log(lam) - std::lgamma(lam + 1.0)) : 0.0;   // host glibc
     }
     a.T = T;
+    a.reject_sum = INFINITY;                                           // early rejection: epipf_abc turns it on
     a.last_day = (double)(T - 1);
     a.f = run_index;
     a.k0 = (uint32_t)key;
@@ -905,6 +906,15 @@ int epipf_abc(epipf_ctx* c, const double* Y, int T, int no_of_samples, double th
     HIP_TRY(hipSetDevice(c->device));
     if (int rc = abc_buffers(c, T, max_batch, no_of_samples, p)) return rc;
     AbcArgs a = p.args;
+    // Early rejection: the device distance is fl(fl(fl(si/T) + fl(sr/T))/2) with si, sr numpy-pairwise
+    // sums of the non-negative terms fl(|x_d - y_d|), so it is at least the exact (sum_I + sum_R)/(2T) times
+    // (1-u)^(T+4), and a lane's running sum `acc` of the same terms is at most that exact sum times (1+u)^(2T+2)
+    // (u = 2^-53).  acc > 2T threshold (1 + 1e-9) therefore proves distance > threshold (for T <= kAbcMaxDays,
+    // (3T+8)u < 2e-10), i.e. the trial is rejected (abc_algo.py:30-33).  Only for a threshold well inside the normal
+    // range (no subnormal quotients); EPIPF_ABC_EARLY=0 turns it off (the results are identical either way).
+    bool early = threshold >= 1e-200 && threshold <= 1e200;
+    if (const char* e = getenv("EPIPF_ABC_EARLY")) early = early && atoi(e) != 0;
+    if (early) a.reject_sum = 2.0 * (double)T * threshold * (1.0 + 1e-9);
     HIP_TRY(hipMemcpyAsync(p.Ydev, Y, sizeof(double) * 3 * (size_t)T, hipMemcpyHostToDevice, c->stream));
     int have = 0;
     int64_t t = 0, last = -1;

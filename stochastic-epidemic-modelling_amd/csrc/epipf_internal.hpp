@@ -132,6 +132,9 @@ struct AbcArgs {
     double last_day;             // T - 1 as a kernel argument (an SGPR pair; a VALU int->f64 convert would not be)
     double prior_lo[2], prior_rng[2];   // lo and hi - lo (numpy uniform's range)
     double lam[3], pm[3];        // initial-count means Y[0].astype(int) and their mode probabilities
+    // early rejection (epipf_abc only): a one-lane trial stops once its running sum of |I_d - Y_I,d| + |R_d - Y_R,d|
+    // over the days passed exceeds this bound, which proves distance > threshold; INFINITY: off
+    double reject_sum;
     int32_t* days;
     double* theta;
     double* dist;

@@ -176,3 +176,47 @@ def test_abc_lane_groups_reference_goldens(abc_golden, monkeypatch, name):
     np.testing.assert_array_equal(r["gamma"], rec["gamma"])
     np.testing.assert_array_equal(r["trajectories"], rec["trajectories"])
     assert r["trials"] == int(rec["trials"])
+
+
+def _abc_both_ways(monkeypatch, engine, Y, n, thr, pr, key, run, **kw):
+    out = {}
+    for early in ("0", "1"):
+        monkeypatch.setenv("EPIPF_ABC_EARLY", early)
+        out[early] = engine.abc(Y, n, thr, pr, key, run, **kw)
+    for a, b in zip(out["0"], out["1"]):
+        np.testing.assert_array_equal(a, b)
+    return out["1"]
+
+
+@pytest.mark.parametrize("name", ABC_CASES)
+def test_abc_early_rejection_changes_nothing(abc_golden, engine, monkeypatch, name):
+    """epipf_abc stops a trial once its partial distance sum proves distance > threshold: accepted
+    draws, trajectories and the trial count are identical with it off (EPIPF_ABC_EARLY=0) and on, and equal the
+    reference's golden run."""
+    rec = abc_golden["abc_" + name]
+    theta, traj, trials, acc = _abc_both_ways(monkeypatch, engine, rec["Y"], int(rec["n"]), float(rec["threshold"]),
+                                              priors_of(rec), int(rec["key"]), int(rec["f"]))
+    assert acc == int(rec["n"]) and trials == int(rec["trials"])
+    np.testing.assert_array_equal(theta[:, 0], rec["beta"])
+    np.testing.assert_array_equal(traj, rec["trajectories"])
+
+
+def test_abc_early_rejection_at_the_threshold(abc_golden, engine, monkeypatch):
+    """Thresholds placed exactly on trial distances (the oracle's): a trial with distance == threshold is accepted
+    (abc_algo.py:30-33), so the early bound must never reject it.  Also the production setting (2000 samples at
+    150, hundreds of thousands of trials) with lane groups on part of small batches."""
+    rec = abc_golden["abc_noisy_150"]
+    Y, pr = rec["Y"], priors_of(rec)
+    _, _, odist, _ = oracle.abc_trials(Y, pr, 77, 2, 0, 4000)
+    srt = np.sort(odist)
+    for k in (5, 40, 400):
+        thr = float(srt[k])
+        theta, traj, trials, acc = _abc_both_ways(monkeypatch, engine, Y, k + 1, thr, pr, 77, 2, batch=1000)
+        assert acc == k + 1
+        last = np.nonzero(~(odist > thr))[0][k]
+        assert trials == last + 1
+        np.testing.assert_array_equal(traj[-1, :, 1:], oracle.abc_trials(Y, pr, 77, 2, last, 1)[1][0])
+    _abc_both_ways(monkeypatch, engine, Y, 2000, 150.0, pr, 2024, 3)
+    monkeypatch.setenv("EPIPF_ABC_LANES", "4")
+    monkeypatch.setenv("EPIPF_ABC_GROUP_FRAC", "0.25")
+    _abc_both_ways(monkeypatch, engine, Y, 300, 150.0, pr, 2024, 4, batch=20000)
