@@ -53,3 +53,30 @@ def test_random_abc_trials_match_oracle(seed):
     np.testing.assert_array_equal(th, oth, err_msg=f"seed {seed}")
     np.testing.assert_array_equal(rows, orows, err_msg=f"seed {seed}")
     np.testing.assert_array_equal(dist, odist, err_msg=f"seed {seed}")
+
+
+@pytest.mark.parametrize("seed", range(max(CASES // 2, 1)))
+def test_random_abc_runs_with_early_rejection_match_oracle(seed, monkeypatch):
+    """Whole epipf_abc runs (batched rejection loop) on the random cases, thresholds placed ON oracle distances so that
+    ties at the threshold decide acceptance: with early rejection on (default) and off, the accepted draws, their day
+    tables and the trial count equal the oracle's first k+1 accepted trials (abc_algo.py:30-33, trial order)."""
+    from epipf.engine import Engine
+    a = _case(seed)
+    rs = np.random.RandomState(7700 + seed)
+    M = 3000
+    oth, orows, odist, _ = oracle.abc_trials(a["Y"], a["pr"], a["key"], a["run"], 0, M)
+    k = int(rs.choice([0, 3, 30, 300]))
+    thr = float(np.sort(odist)[k])
+    acc_idx = np.nonzero(~(odist > thr))[0][:k + 1]
+    batch = int(rs.choice([0, 700, 5000]))
+    eng = Engine("sir", 1, 1, 1, 1)
+    try:
+        for early in ("1", "0"):
+            monkeypatch.setenv("EPIPF_ABC_EARLY", early)
+            theta, traj, trials, acc = eng.abc(a["Y"], k + 1, thr, a["pr"], a["key"], a["run"], batch=batch)
+            msg = f"seed {seed} early {early} k {k} thr {thr}"
+            assert acc == k + 1 and trials == int(acc_idx[-1]) + 1, msg
+            np.testing.assert_array_equal(theta, oth[acc_idx], err_msg=msg)
+            np.testing.assert_array_equal(traj[:, :, 1:], orows[acc_idx].astype(np.float64), err_msg=msg)
+    finally:
+        eng.close()
