@@ -92,6 +92,8 @@ struct epipf_ctx {
     int abc_lanes = 0;
     double abc_group_frac = 0.5, abc_frac = 0.5;   // share of the sorted trials on lane groups (EPIPF_ABC_GROUP_FRAC)
     bool fast_ssa = true;    // certified f32 event loop (EPIPF_SSA_FAST=0 disables; results are identical)
+    bool seq_decide = false; // lane groups: the sequential decision pass instead of the fixed-point one
+                             // (EPIPF_GROUP_DECIDE=seq; results are identical, A/B and tests)
     float clock_slack = 1.f; // EPIPF_CLOCK_SLACK >= 1 widens its clock band: replays on purpose (stress tests)
     float band_slack = 1.f;  // EPIPF_BAND_SLACK >= 1 widens the channel decision's band: exact decisions and redone
                              // lane-group chunks on purpose (stress tests)
@@ -227,6 +229,7 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     c->max_chains = max_chains;
     c->wg = default_wg(n_particles);
     if (const char* e = getenv("EPIPF_SSA_FAST")) c->fast_ssa = atoi(e) != 0;
+    if (const char* e = getenv("EPIPF_GROUP_DECIDE")) c->seq_decide = strcmp(e, "seq") == 0;
     if (const char* e = getenv("EPIPF_CLOCK_SLACK")) c->clock_slack = std::max(1.0f, std::min(1e6f, (float)atof(e)));
     if (const char* e = getenv("EPIPF_BAND_SLACK")) c->band_slack = std::max(1.0f, std::min(1e4f, (float)atof(e)));
     if (const char* e = getenv("EPIPF_TIE_SCALE")) c->tie_scale = std::max(1.0, std::min(1e300, atof(e)));
@@ -378,7 +381,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
         q.k0 = (uint32_t)keys[ch];
         q.k1 = (uint32_t)(keys[ch] >> 32);
         q.f = filter_index[ch];
-        q.flags = c->fast_ssa ? kChainFastSsa : 0u;
+        q.flags = (c->fast_ssa ? kChainFastSsa : 0u) | (c->seq_decide ? kChainSeqDecide : 0u);
         q.clock_slack = c->clock_slack;
         q.band_slack = c->band_slack;
         c->h_status[ch] = on ? EPIPF_STATUS_OK : EPIPF_STATUS_SKIPPED;
@@ -567,7 +570,7 @@ int epipf_simulate(epipf_ctx* c, int n, const int32_t* states_in, const double* 
     memset(&q, 0, sizeof q);
     for (int i = 0; i < d; ++i) { q.theta[i] = theta[i]; q.thetaf[i] = (float)theta[i]; }
     q.k0 = (uint32_t)key; q.k1 = (uint32_t)(key >> 32); q.f = filter_index;
-    q.flags = c->fast_ssa ? kChainFastSsa : 0u;
+    q.flags = (c->fast_ssa ? kChainFastSsa : 0u) | (c->seq_decide ? kChainSeqDecide : 0u);
     q.clock_slack = c->clock_slack;
     q.band_slack = c->band_slack;
     HIP_TRY(hipMemcpyAsync(dcp, &q, sizeof q, hipMemcpyHostToDevice, c->stream));

@@ -99,6 +99,7 @@ struct ChainParam {
                                // same results); tests only
 };
 constexpr uint32_t kChainFastSsa = 1u;   // (all models)
+constexpr uint32_t kChainSeqDecide = 2u; // lane groups: sequential decision pass (EPIPF_GROUP_DECIDE=seq; A/B, tests)
 
 // ------------------------------------------------------------------------------- reference-exact log
 // glibc 2.35 log(x), the function behind the reference's draws (numpy legacy exponential = scale * -log(1 - U),
@@ -469,6 +470,20 @@ struct FastSsa<kSIR, 1> {                                              // gilles
         S = S - (rec ? 0.f : 1.f);
         I = I + (rec ? -1.f : 1.f);
     }
+    // The lane-group fixed-point pass (epipf_group.hpp: decide_fixed_point): this lane's event decided on its own, on
+    // decide_lo's Tlo side, as an event count in a byte field (byte 0 infections, byte 1 recoveries), and a state
+    // rebuilt from the chunk start b and the counts n of the events before it (small integers: exact in f32)
+    static constexpr bool kFixedPoint = true;
+    __device__ __forceinline__ uint32_t outcome(float ulo) const {
+        float c[1];
+        const float Tlo = ulo * cum(c);
+        return c[0] < Tlo ? 0x100u : 0x1u;
+    }
+    __device__ __forceinline__ void advance(const FastSsa& b, uint32_t n) {
+        const float ni = (float)(n & 0xFFu), nr = (float)((n >> 8) & 0xFFu);
+        S = b.S - ni;
+        I = (b.I + ni) - nr;
+    }
     __device__ __forceinline__ int save(double* x) const {
         const float inf = S0 - S, rec = SI0 - (S + I);
         x[0] = (double)S; x[1] = (double)I; x[2] = x[2] + (double)rec;
@@ -518,6 +533,19 @@ struct FastSsa<kSEIR, 1> {                                             // gilles
         S = S - (b0 ? 0.f : 1.f);
         E = E + (b0 ? (b1 ? 0.f : -1.f) : 1.f);
         I = I + (b1 ? -1.f : (b0 ? 1.f : 0.f));
+    }
+    // fixed-point pass (see FastSsa<kSIR>): byte 0 S->E, byte 1 E->I, byte 2 I->R
+    static constexpr bool kFixedPoint = true;
+    __device__ __forceinline__ uint32_t outcome(float ulo) const {
+        float c[2];
+        const float Tlo = ulo * cum(c);
+        return c[1] < Tlo ? 0x10000u : c[0] < Tlo ? 0x100u : 0x1u;
+    }
+    __device__ __forceinline__ void advance(const FastSsa& b, uint32_t n) {
+        const float n0 = (float)(n & 0xFFu), n1 = (float)((n >> 8) & 0xFFu), n2 = (float)((n >> 16) & 0xFFu);
+        S = b.S - n0;
+        E = (b.E + n0) - n1;
+        I = (b.I + n1) - n2;
     }
     __device__ __forceinline__ int save(double* x) const {
         const float n0 = S0 - S, n2 = SEI0 - ((S + E) + I), n1 = (I - I0) + n2;
@@ -796,6 +824,36 @@ struct FastSubgroupsPacked {                                           // gilles
             }
             S2[p] = S2[p] - ds;
             I2[p] = I2[p] + di;
+        }
+    }
+    // fixed-point pass (see FastSsa<kSIR>): byte r infections of group r, byte G + r recoveries of group r; four byte
+    // fields, so G <= 2 (larger G keeps the sequential pass)
+    static constexpr bool kFixedPoint = 2 * G <= 4;
+    static constexpr uint32_t code(int ch) {             // the event count of channel ch, in its field
+        return 1u << (8 * (ch % (G + 1) < G ? ch % (G + 1) : G + ch / (G + 1)));
+    }
+    __device__ __forceinline__ uint32_t outcome(float ulo) const {
+        float c[NCH - 1];
+        const float Tlo = ulo * cum(c);
+        uint32_t d = code(0);                            // channel = #{i : c_i < Tlo} (the c_i are nondecreasing)
+#pragma unroll
+        for (int i = 0; i < NCH - 1; ++i) d = c[i] < Tlo ? code(i + 1) : d;
+        return d;
+    }
+    __device__ __forceinline__ void advance(const FastSubgroupsPacked& b, uint32_t n) {
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            f2 ni{0.f, 0.f}, nr{0.f, 0.f};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int r = 2 * p + h;
+                if (r < G) {
+                    ni[h] = (float)((n >> (8 * r)) & 0xFFu);
+                    nr[h] = (float)((n >> (8 * (G + r))) & 0xFFu);
+                }
+            }
+            S2[p] = b.S2[p] - ni;
+            I2[p] = (b.I2[p] + ni) - nr;
         }
     }
     __device__ __forceinline__ int save(double* x) const {

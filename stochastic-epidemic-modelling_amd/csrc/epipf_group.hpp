@@ -101,6 +101,19 @@ __device__ __forceinline__ void decide_lo(F& st, float ulo) {
     st.apply_below(below);
 }
 
+// The chunk's decisions in event order (rounds 2-3): event e's uniform broadcast to the group, decide_lo applied to
+// the group's state; lane e % W keeps the state before event e.
+template <int W, int K, class F>
+__device__ __forceinline__ void decide_sequential(F& st, F* mine, const float* ulo, int gl) {
+    auto decide = [&](auto I) __attribute__((always_inline)) -> bool {
+        constexpr int e = decltype(I)::value;
+        mine[e / W].keep_if(gl == e % W, st);
+        decide_lo(st, __uint_as_float(group_lane_dpp<W, e % W>(__float_as_uint(ulo[e / W]))));
+        return true;
+    };
+    StaticFor<0, W * K>::run(decide);
+}
+
 template <typename F>
 __device__ __forceinline__ bool event_certified(const F& s, float ulo, float kB) {
     constexpr int NCH = F::NCH;
@@ -111,6 +124,55 @@ __device__ __forceinline__ bool event_certified(const F& s, float ulo, float kB)
 #pragma unroll
     for (int i = 0; i < NCH - 1; ++i) sure = sure && ((c[i] < Tlo) == (c[i] < Thi));
     return sure || !s.active();
+}
+
+// Inclusive prefix sum over this lane's group of W consecutive lanes (Hillis-Steele on DPP row shifts; a group of
+// W <= 16 lies inside one DPP row, whose edge reads 0; for W < 16 a lane whose source lies in the group before it adds
+// nothing: a select on a constant lane mask).
+constexpr uint64_t group_tail_mask(int W, int k) {     // lanes with (lane % W) >= k
+    uint64_t m = 0;
+    for (int l = 0; l < 64; ++l) m |= (uint64_t)((l % W) >= k) << l;
+    return m;
+}
+
+template <int W>
+__device__ __forceinline__ uint32_t group_inclusive_scan(uint32_t v) {
+    auto level = [&](auto KK) __attribute__((always_inline)) {
+        constexpr int k = decltype(KK)::value;
+        if constexpr (k < W) {
+            uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + k, 0xF, 0xF, true);   // row_shr:k
+            if constexpr (W < 16) t = __builtin_amdgcn_inverse_ballot_w64(group_tail_mask(W, k)) ? t : 0u;
+            v += t;
+        }
+    };
+    level(std::integral_constant<int, 1>{});
+    level(std::integral_constant<int, 2>{});
+    level(std::integral_constant<int, 4>{});
+    level(std::integral_constant<int, 8>{});
+    return v;
+}
+
+// The chunk's channel decisions as a fixed point (round 4), instead of W dependent decisions in event order.  With
+// d_e = f_e(x_e) the decision of event e on the state x_e before it (decide_lo's Tlo side: F::outcome) and
+// x_e = x_0 + sum_{k<e} delta(d_k), guesses g are iterated as g'_e = f_e(x_0 + sum_{k<e} delta(g_k)), all events at
+// once (one lane each), starting from g_e = f_e(x_0).  By induction the first k events of the k-th iterate equal the
+// sequential pass's, so at most W + 1 evaluations reach it, and a guess that reproduces itself IS the sequential
+// pass's result: g_0 = f_0(x_0) = d_0, and g_k = d_k for k < e gives g_e = f_e(x_e) = d_e.  The events' count
+// vectors (F::outcome's byte fields) are summed by a group prefix scan.  A chunk's state moves too little for most
+// decisions to change: at config 5 (G = 2, W = 8) 96% of the chunks confirm on the second evaluation and a wave's
+// slowest group needs 2.3 evaluations on average -- against 8 dependent decisions of the sequential pass.
+// On return: mine = the state before this lane's event, st = the state after the chunk (every lane of the group).
+template <int W, class F>
+__device__ __forceinline__ void decide_fixed_point(F& st, F& mine, float ulo) {
+    uint32_t d = st.outcome(ulo), ex = 0;
+    for (int it = 0; it <= W; ++it) {                    // <= W + 1 evaluations (see above); exits by the break
+        ex = group_inclusive_scan<W>(d) - d;
+        mine.advance(st, ex);
+        const uint32_t d2 = mine.outcome(ulo);
+        if (!__any(d2 != d)) break;                      // wave-uniform: every group reproduced its guess
+        d = d2;
+    }
+    st.advance(st, group_lane_dpp<W, W - 1>(ex + d));
 }
 
 // 1/sum(a) of the exact state (the reference's expressions, SsaState::rates)
@@ -217,13 +279,15 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         __builtin_amdgcn_sched_barrier(0);
         EPIPF_PHASE_MARK(tB);
         const F st0 = st;
-        auto decide = [&](auto I) __attribute__((always_inline)) -> bool {
-            constexpr int e = decltype(I)::value;
-            mine[e / W].keep_if(gl == e % W, st);
-            decide_lo(st, __uint_as_float(group_lane_dpp<W, e % W>(__float_as_uint(ulo[e / W]))));
-            return true;
-        };
-        StaticFor<0, E>::run(decide);
+        if constexpr (F::kFixedPoint && K == 1) {
+            if (!(cp.flags & kChainSeqDecide)) {
+                decide_fixed_point<W>(st, mine[0], ulo[0]);
+            } else {
+                decide_sequential<W, K>(st, mine, ulo, gl);
+            }
+        } else {
+            decide_sequential<W, K>(st, mine, ulo, gl);
+        }
         bool uncertified = false;                        // this lane's events, on the states before them
 #pragma unroll
         for (int k = 0; k < K; ++k) uncertified = uncertified || !event_certified(mine[k], ulo[k], kB);
