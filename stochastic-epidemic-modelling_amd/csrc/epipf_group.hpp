@@ -161,18 +161,36 @@ __device__ __forceinline__ uint32_t group_inclusive_scan(uint32_t v) {
 // vectors (F::outcome's byte fields) are summed by a group prefix scan.  A chunk's state moves too little for most
 // decisions to change: at config 5 (G = 2, W = 8) 96% of the chunks confirm on the second evaluation and a wave's
 // slowest group needs 2.3 evaluations on average -- against 8 dependent decisions of the sequential pass.
-// On return: mine = the state before this lane's event, st = the state after the chunk (every lane of the group).
-template <int W, class F>
-__device__ __forceinline__ void decide_fixed_point(F& st, F& mine, float ulo) {
-    uint32_t d = st.outcome(ulo), ex = 0;
-    for (int it = 0; it <= W; ++it) {                    // <= W + 1 evaluations (see above); exits by the break
-        ex = group_inclusive_scan<W>(d) - d;
-        mine.advance(st, ex);
-        const uint32_t d2 = mine.outcome(ulo);
-        if (!__any(d2 != d)) break;                      // wave-uniform: every group reproduced its guess
-        d = d2;
+// With K events per lane (event k W + gl in slot k) the K slots' counts are scanned side by side and slot k's prefix is
+// offset by the totals of the slots before it.
+// On return: mine[k] = the state before event k W + gl, st = the state after the chunk (every lane of the group).
+template <int W, int K, class F>
+__device__ __forceinline__ void decide_fixed_point(F& st, F* mine, const float* ulo) {
+    uint32_t d[K], ex[K], total = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) d[k] = st.outcome(ulo[k]);
+    for (int it = 0; it <= W * K; ++it) {                // <= W K + 1 evaluations (see above); exits by the break
+        uint32_t incl[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) incl[k] = group_inclusive_scan<W>(d[k]);
+        total = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            ex[k] = total + (incl[k] - d[k]);
+            if (k + 1 < K) total += group_lane_dpp<W, W - 1>(incl[k]);
+            else total = group_lane_dpp<W, W - 1>(ex[k] + d[k]);
+        }
+        bool changed = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            mine[k].advance(st, ex[k]);
+            const uint32_t d2 = mine[k].outcome(ulo[k]);
+            changed = changed || d2 != d[k];
+            d[k] = d2;
+        }
+        if (!__any(changed)) break;                      // wave-uniform: every group reproduced its guess
     }
-    st.advance(st, group_lane_dpp<W, W - 1>(ex + d));
+    st.advance(st, total);
 }
 
 // 1/sum(a) of the exact state (the reference's expressions, SsaState::rates)
@@ -279,9 +297,9 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         __builtin_amdgcn_sched_barrier(0);
         EPIPF_PHASE_MARK(tB);
         const F st0 = st;
-        if constexpr (F::kFixedPoint && K == 1) {
+        if constexpr (F::kFixedPoint) {
             if (!(cp.flags & kChainSeqDecide)) {
-                decide_fixed_point<W>(st, mine[0], ulo[0]);
+                decide_fixed_point<W, K>(st, mine, ulo);
             } else {
                 decide_sequential<W, K>(st, mine, ulo, gl);
             }
@@ -531,7 +549,7 @@ static void launch_group_t(const StepArgs& a, int p, dim3 grid, size_t lds, hipS
 }
 
 // (lanes per particle W, events per lane per chunk K) instantiated
-#define EPIPF_GROUP_SHAPES(X) X(2, 1) X(4, 1) X(8, 1) X(16, 1)
+#define EPIPF_GROUP_SHAPES(X) X(2, 1) X(4, 1) X(8, 1) X(16, 1) X(4, 2) X(8, 2) X(16, 2)
 
 template <int MODEL, int G, int OBS>
 static GroupStepFn pick_wk(int W, int K) {

@@ -11,7 +11,7 @@ import oracle
 pytestmark = pytest.mark.gpu
 
 LANES = [1, 2, 4, 8, 16]
-SHAPES = [(2, 1), (4, 1), (8, 1), (16, 1)]   # (W, K) instantiated
+SHAPES = [(2, 1), (4, 1), (8, 1), (16, 1), (4, 2), (8, 2), (16, 2)]   # (W, K) instantiated
 
 
 def _case(datasets_golden, model):
@@ -100,6 +100,30 @@ def test_every_lane_shape_matches_oracle(datasets_golden, model, shape):
     np.testing.assert_array_equal(hid[0], o["hidden"])
     np.testing.assert_array_equal(anc[0], o["ancestry"])
     np.testing.assert_allclose(lz[0], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.parametrize("shape", [(4, 1), (8, 1), (8, 2)])
+@pytest.mark.parametrize("decide", ["seq", "fixed_point"])
+@pytest.mark.parametrize("model", ["sir", "seir", "sir_subgroups", "sir_subgroups2"])
+def test_decision_passes_equal_oracle_with_widened_band(datasets_golden, monkeypatch, model, decide, shape):
+    """Both lane-group decision passes -- the fixed-point one (round 4: every event of a chunk decided at once, iterated
+    to the sequential pass's result) and the sequential one it replaced (EPIPF_GROUP_DECIDE=seq) -- with the band
+    widened 3000x so that chunks are also redone on the exact fallback: states, ancestors and likelihoods are the
+    oracle's."""
+    monkeypatch.setenv("EPIPF_BAND_SLACK", "3000")
+    if decide == "seq":
+        monkeypatch.setenv("EPIPF_GROUP_DECIDE", "seq")
+    c = _case(datasets_golden, model)
+    W, K = shape
+    lz, st, hid, anc, used = _run(model, c, 500, 2, W, [51, 52], [3, 8], events=K)
+    assert used == W
+    for ch in range(2):
+        o = oracle.particle_filter(c["Y"], model, c["theta"], c["obs"], c["probs"], 500, c["npop"], c["mu"],
+                                   key=[51, 52][ch], filter_index=[3, 8][ch])
+        assert int(st[ch]) == o["status"] == 0
+        np.testing.assert_array_equal(hid[ch], o["hidden"])
+        np.testing.assert_array_equal(anc[ch], o["ancestry"])
+        np.testing.assert_allclose(lz[ch], o["log_zetas"], rtol=1e-12, atol=1e-9)
 
 
 @pytest.mark.parametrize("G", [3, 4])
