@@ -10,9 +10,13 @@ own `--chains` chains with no collective on the data path; the posterior draws o
 all-gathered over RCCL at the end of the timed region (pmcmc chain gather).
 
 Also reported: roofline of the dominant kernel (pf_step_kernel, HIP-event timed on the engine's stream),
-and a CPU baseline (the oracle C restatement, OpenMP, on a bounded sample) on rank 0 at N=1.
+a CPU baseline (the oracle C restatement, OpenMP, on a bounded sample) on rank 0 at N=1, and `configs`: short
+timed runs of the other BASELINE workloads -- configs 3, 4, 5 at 256 chains per GPU and config 5 at ONE chain per GPU
+(BASELINE's "8 independent chains across 8 GPUs" layout, the lane-group kernel) -- each with its own roofline where a
+PMC profile of that (config, chains, lanes) on this library build is committed (profiles/pmc_*.json).
 """
 import argparse
+import glob
 import json
 import os
 import platform
@@ -27,22 +31,31 @@ sys.path.insert(0, os.path.join(REPO, "stochastic-epidemic-modelling_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters
 VALU_PEAK = 1024 * 2.4e9 / 2   # wave64 VALU instructions/s: 1024 SIMDs, 2.4 GHz, one wave64 instruction per 2 cycles
 MODEL_NAMES = {"sir": "SIR", "seir": "SEIR", "sir_subgroups": "multi-subgroup SIR", "sir_subgroups2": "SIR subgroups2"}
+# the `configs` workloads: name -> (BASELINE config, chains per GPU)
+CONFIG_RUNS = {"3": (3, 256), "4": (4, 256), "5": (5, 256), "5x1": (5, 1)}
 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    # under a launcher (WORLD_SIZE set) --gpus defaults to the world size; without one, to 1
+    ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--chains", type=int, default=int(os.environ.get("EPIPF_BENCH_CHAINS", 256)),
                     help="independent MH chains per GPU (batched in one launch per filter step)")
     ap.add_argument("--particles", type=int, default=None, help="default: the config's N (SURVEY.md §8d)")
     ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--proposal", choices=["config", "fixed_theta"], default="config",
+                    help="MH proposal h * sigma: the config's (epipf.datasets.PROPOSALS) or h = 1e-4, sigma = I")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--single-chain", action=argparse.BooleanOptionalAction, default=True,
                     help="also time 1 chain/GPU (N=1 only): one filter per MH iteration, and speculative MH (extra fields)")
+    ap.add_argument("--configs", default="3,4,5,5x1",
+                    help="extra timed workloads for the `configs` object (comma list of " + ", ".join(CONFIG_RUNS) +
+                         "; 'none' to skip)")
+    ap.add_argument("--configs-steps", type=int, default=4, help="timed MH iterations per `configs` workload")
     ap.add_argument("--pipelines", type=int, default=int(os.environ.get("EPIPF_BENCH_PIPELINES", 0)),
                     help="chain groups on their own engine + host thread, so each group's MH host work overlaps the "
                          "others' filters (epipf.pmcmc.run_pipelined); 1 = one lockstep sampler; 0 = automatic: 2 "
@@ -158,16 +171,290 @@ def launch_ranks(args, argv):
     return subprocess.call(cmd, env=dict(os.environ, EPIPF_BENCH_LAUNCHED="1"))
 
 
+def resolve_gpus(args, env):
+    """--gpus against the launcher's WORLD_SIZE: absent -> the world size (1 without a launcher); an explicit value
+    that differs from a launcher's world size is an error (returns a message), as one rank per GPU is the contract."""
+    world = int(env["WORLD_SIZE"]) if "WORLD_SIZE" in env else None
+    if args.gpus is None:
+        args.gpus = world or 1
+        return None
+    if world is not None and world != args.gpus:
+        return f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}"
+    return None
+
+
+class Ctx:
+    """Rank context shared by the timed runs."""
+
+    def __init__(self, world, rank, local, dist, force_dist, backend):
+        self.world, self.rank, self.local = world, rank, local
+        self.dist, self.force_dist, self.backend = dist, force_dist, backend
+
+    def barrier(self):
+        import torch
+        if self.dist is not None:
+            self.dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_sum(self, dt, filters):
+        """(max over ranks of dt, sum over ranks of filters)."""
+        if self.dist is None:
+            return dt, filters
+        import torch
+        tt = torch.tensor([dt, float(filters)], dtype=torch.float64,
+                          device=f"cuda:{self.local}" if self.backend == "nccl" else "cpu")
+        self.dist.all_reduce(tt[0:1], op=self.dist.ReduceOp.MAX)
+        self.dist.all_reduce(tt[1:2], op=self.dist.ReduceOp.SUM)
+        return float(tt[0]), int(tt[1])
+
+
+def proposal(meta, kind):
+    """(h, sigma, description) of the MH random walk: the config's own (epipf.datasets.PROPOSALS) or fixed_theta."""
+    if kind == "fixed_theta":
+        from epipf.datasets import FIXED_THETA
+        return FIXED_THETA["h"], FIXED_THETA["sigma"], FIXED_THETA["proposal"]
+    return meta["h"], meta["sigma"], meta["proposal"]
+
+
+def timed_chains(ctx, args, cfg, chains, steps, warmup, kind, pipelines=1, streams_env=4):
+    """`chains` independent MH chains per rank of BASELINE config `cfg`: warmup, then `steps` timed MH iterations
+    between barriers (+ the end-of-run RCCL all-gather of the draws), then one untimed iteration with the device
+    counters on.  Returns a dict of what the bench line reports."""
+    from epipf import _lib, datasets
+    from epipf.distributed import gather_draws, pack_draws, shard
+    from epipf.engine import Engine
+    from epipf.pmcmc import ChainSampler, chain_key, run_pipelined
+    Y, meta = datasets.benchmark_dataset(cfg)
+    N, T = (args.particles if cfg == args.config and args.particles else meta["N"]), Y.shape[0]
+    h, sigma, pdesc = proposal(meta, kind)
+    gid = shard(chains * ctx.world, ctx.world, ctx.rank)              # global chain ids of this rank
+    P = max(1, min(pipelines, chains))
+    samplers = []
+    for k in range(P):                                               # contiguous chain groups, one engine each
+        ids = gid[k * chains // P:(k + 1) * chains // P]
+        kw = {}
+        if P > 1:
+            eng_k = Engine(meta["model"], len(np.atleast_1d(meta["n_population"])), N, T, len(ids), device=ctx.local)
+            eng_k.set_streams(max(1, streams_env // P))
+            kw["engine"] = eng_k
+        samplers.append(ChainSampler(Y, meta["model"], list(meta["theta"]), h, sigma=sigma,
+                                     iters=warmup + steps + 2, observations=meta.get("observations", False),
+                                     probs=meta["probs"], n_particles=N, n_population=meta["n_population"],
+                                     mu=meta["mu"], rngs=[np.random.RandomState(args.seed + g) for g in ids],
+                                     keys=[chain_key(args.seed, g) for g in ids], device=ctx.local, mh_ratio="log",
+                                     **kw))
+    engines = [s.eng for s in samplers]
+    streams = P * max(1, streams_env // P) if P > 1 else min(streams_env, chains)   # concurrent step launches
+    for s_ in samplers:
+        s_.initialise()
+    run_pipelined(samplers, warmup) if P > 1 else [samplers[0].step() for _ in range(warmup)]
+
+    def stats_sum():
+        tot = {}
+        for e in engines:
+            for k_, v in e.stats().items():
+                tot[k_] = tot.get(k_, 0) + v
+        return tot
+
+    def accept_counts():
+        return sum(a for s_ in samplers for a in s_.acceptances), sum(f for s_ in samplers for f in s_.filters_run)
+
+    for e in engines:
+        e.reset_stats()
+        e.set_profiling(_lib.PROFILE_TIMING)     # HIP events only: the timed kernels are the production ones
+    a0, f0 = accept_counts()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    if P > 1:
+        filters = run_pipelined(samplers, steps)
+    else:
+        filters = sum(samplers[0].step() for _ in range(steps))
+    # end of run: gather every rank's posterior draws over RCCL (xGMI), SURVEY.md §8e
+    results = [r for s_ in samplers for r in s_.results()]
+    gathered = gather_draws(pack_draws(results, upto=samplers[0].i), ctx.local, force=ctx.force_dist)
+    ctx.barrier()
+    dt = time.perf_counter() - t0
+    a1, f1 = accept_counts()
+    st = stats_sum()
+    # one extra, untimed MH iteration with device counters on: SSA events/s and SIMD lane use
+    for e in engines:
+        e.reset_stats()
+        e.set_profiling(_lib.PROFILE_COUNTERS)
+    run_pipelined(samplers, 1) if P > 1 else samplers[0].step()
+    for e in engines:
+        e.set_profiling(_lib.PROFILE_OFF)
+    cst = stats_sum()
+    dt_max, filters_all = ctx.max_sum(dt, filters)
+    lanes = int(engines[0].stats()["last_lanes"]) or 1
+    return dict(Y=Y, meta=meta, N=N, T=T, chains=chains, P=P, streams=streams, samplers=samplers, engines=engines,
+                dt=dt_max, filters=filters, filters_all=filters_all, value=filters_all * N * T / dt_max, st=st, cst=cst,
+                lanes=lanes, h=h, sigma=sigma, proposal=pdesc, gathered=gathered,
+                acceptance_rate=(a1 - a0) / max(1, f1 - f0), steps=steps, warmup=warmup)
+
+
+def n_comp(meta):
+    return {"sir": 3, "seir": 4}.get(meta["model"], 3 * len(np.atleast_1d(meta["n_population"])))
+
+
+def pmc_profile(cfg, chains, lanes):
+    """The committed PMC pass of this (config, chains per GPU, lanes per particle) on the library timed here
+    (profiles/pmc_*.json, written by scripts/parse_rocprof.py; matched on the library's build id -- a hash of every
+    kernel source and flag, epipf_build_id -- so after any kernel change it reads as stale and the PMC fields are
+    null).  Returns (profile, path) or ({}, None)."""
+    from epipf import _lib
+    bid = _lib.build_id()
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
+        try:
+            p = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if (p.get("build_id") == bid and p.get("config", 2) == cfg and p.get("chains_per_gpu", 256) == chains
+                and p.get("lanes", 1) == lanes):
+            return p, os.path.relpath(path, REPO)
+    return {}, None
+
+
+def roofline(run, value):
+    """Roofline of the run's dominant kernel: pf_step_kernel (one lane per particle) or pf_step_group_kernel (W lanes
+    per particle).  Both are bound by vector-instruction issue (the SSA event loop), not by HBM: the
+    primary roofline is VALU issue, from the committed PMC pass's SQ_INSTS_VALU per particle-step x the live rate;
+    the HBM figures the north star asks for are in `hbm` (algorithmic 8C + 40 B per particle-step over the launch
+    duration)."""
+    st, meta, N = run["st"], run["meta"], run["N"]
+    lanes = run["lanes"]
+    steps = run["steps"]
+    launches = max(1, st["step_kernel_launches"])
+    avg_launch_s = st["step_kernel_ms"] / 1e3 / launches
+    step_wall_s = st["step_ms"] / 1e3 / max(1, st["step_launches"])
+    units_per_launch = run["filters"] * N / steps / run["streams"]   # particle-steps per kernel launch
+    bytes_per_unit = 8 * n_comp(meta) + 40                            # 8C+40 B per particle-step (DESIGN.md §6)
+    live_gbs = units_per_launch * bytes_per_unit / avg_launch_s / 1e9
+    # chip level: algorithmic bytes of every particle-step of the timed region over its wall time
+    chip_gbs = run["filters"] * N * run["T"] * bytes_per_unit / run["dt"] / 1e9
+    pmc, pmc_path = pmc_profile(run["cfg"], run["chains"], lanes)
+    traffic = traffic_raw = valu = rocprof_us = None
+    if pmc:
+        # MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE counts half the bytes of a coalesced read stream, so
+        # `traffic` doubles the read side (FETCH x 2 + WRITE); the raw counter sum is `traffic_raw`
+        per_unit = pmc.get("hbm_bytes_per_particle_step_read_doubled")
+        traffic = per_unit * units_per_launch if per_unit else None
+        raw_unit = pmc.get("hbm_bytes_per_particle_step")
+        traffic_raw = raw_unit * units_per_launch if raw_unit else None
+        rocprof_us = pmc.get("trace_avg_us")
+        ins = pmc.get("pmc_avg_per_launch", {}).get("SQ_INSTS_VALU")
+        units = pmc.get("particle_steps_per_launch")
+        if ins and units:
+            per_ps = ins / units
+            valu = {"achieved": per_ps * value, "instr_per_particle_step": per_ps,
+                    "cycles_per_instr_at_2.4GHz": VALU_PEAK * 2 / (per_ps * value),
+                    # VALU pipe busy per SIMD-cycle, SQ_ACTIVE_INST_VALU / GRBM_GUI_ACTIVE of the PMC pass
+                    # (dispatches serialised there, so each carries its own launch tail)
+                    "pmc_valu_busy_frac": pmc.get("valu_busy_frac")}
+    hbm_us = rocprof_us or avg_launch_s * 1e6
+    hbm_gbs = units_per_launch * bytes_per_unit / (hbm_us / 1e6) / 1e9
+    hbm = {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
+           "duration_source": f"rocprofv3 average kernel duration ({pmc_path})" if rocprof_us
+           else "HIP events (launch to completion)",
+           "frac_hip_event_span": live_gbs / HBM_PEAK_GBS, "chip_level_frac": chip_gbs / HBM_PEAK_GBS,
+           "bytes_per_particle_step": bytes_per_unit, "traffic": traffic, "traffic_raw": traffic_raw}
+    kernel = "pf_step_kernel" if lanes == 1 else f"pf_step_group_kernel (W={lanes})"
+    return {"bound": "valu", "kernel": kernel,
+            "achieved": valu["achieved"] if valu else None, "peak": VALU_PEAK,
+            "unit": "wave64 VALU instr/s", "frac": valu["achieved"] / VALU_PEAK if valu else None,
+            "traffic": traffic, "valu_issue": valu, "hbm": hbm,
+            "avg_launch_us": avg_launch_s * 1e6, "particle_steps_per_launch": units_per_launch,
+            "concurrent_launches_per_step": run["streams"], "step_wall_us": step_wall_s * 1e6,
+            # the same kernel's average dispatch duration in the committed rocprofv3 trace of this workload; the
+            # HIP-event figure above also counts the time a launch waits for CUs held by concurrent chain-group launches
+            "rocprof_avg_launch_us": rocprof_us,
+            "pmc_profile": {"path": pmc_path, "build_id": pmc.get("build_id")}}
+
+
+def run_summary(run):
+    cst = run["cst"]
+    ps = cst["particle_steps"]
+    return {"value": run["value"], "unit": "particle-steps/s", "ms_per_step": run["dt"] * 1e3 / run["steps"],
+            "steps": run["steps"], "warmup": run["warmup"], "chains_per_gpu": run["chains"],
+            "particles": run["N"], "T_obs": run["T"], "lanes_per_particle": run["lanes"],
+            "kernel": "pf_step_kernel" if run["lanes"] == 1 else "pf_step_group_kernel",
+            "h": run["h"], "proposal": run["proposal"], "acceptance_rate": run["acceptance_rate"],
+            "events_per_particle_step": cst["events"] / ps if ps else None,
+            "events_per_s": run["value"] * cst["events"] / ps if ps else None}
+
+
+def prefetch_chain(args, Y, meta, N, T, local, slots, iters, h=1e-4, sigma=None):
+    """One chain with speculative MH (epipf.prefetch): filters of future iterations share one batched launch sequence;
+    only filters on the realised path count.  slots = "auto" lets the sampler size its rounds."""
+    import torch
+    from epipf.pmcmc import chain_key
+    from epipf.prefetch import PrefetchSampler
+    s2 = PrefetchSampler(Y, meta["model"], list(meta["theta"]), h, sigma=sigma, iters=iters + 40, probs=meta["probs"],
+                         observations=meta.get("observations", False), n_particles=N,
+                         n_population=meta["n_population"], mu=meta["mu"],
+                         rngs=[np.random.RandomState(args.seed)], keys=[chain_key(args.seed, 0)], device=local,
+                         mh_ratio="log", slots=slots)
+    s2.initialise()
+    while s2.i < 20:
+        s2.advance()
+    torch.cuda.synchronize()
+    i0, f0, r0, sp0, a0 = s2.i, s2.filters_run[0], s2.rounds, s2.speculative_filters, s2.acceptances[0]
+    t2 = time.perf_counter()
+    while s2.i < i0 + iters:
+        s2.advance()
+    torch.cuda.synchronize()
+    dt2 = time.perf_counter() - t2
+    return {"value": (s2.filters_run[0] - f0) * N * T / dt2, "slots": slots, "slots_used": s2.slots,
+            "iterations": s2.i - i0, "rounds": s2.rounds - r0,
+            "iterations_per_round": (s2.i - i0) / max(1, s2.rounds - r0),
+            "filters_evaluated": s2.speculative_filters - sp0,
+            "acceptance_rate": (s2.acceptances[0] - a0) / max(1, s2.filters_run[0] - f0),
+            "ms_per_iteration": dt2 * 1e3 / max(1, s2.i - i0)}
+
+
+def config_runs(ctx, args):
+    """The `configs` object: short timed runs of the other BASELINE workloads on every rank (one rank per GPU; the
+    config-5 one-chain entry is BASELINE's 8-chain layout at 8 GPUs), at the config's own proposal and at
+    fixed_theta where that differs."""
+    names = [] if args.configs.strip().lower() in ("", "none") else [c.strip() for c in args.configs.split(",")]
+    out = {}
+    for name in names:
+        if name not in CONFIG_RUNS:
+            raise SystemExit(f"bench.py: unknown --configs entry {name!r}")
+        cfg, chains = CONFIG_RUNS[name]
+        steps = args.configs_steps * (5 if chains == 1 else 1)        # one-chain MH iterations are short
+        entry = None
+        for kind in ("config", "fixed_theta"):
+            run = timed_chains(ctx, args, cfg, chains, steps, 1 if chains > 1 else 2, kind)
+            run["cfg"] = cfg
+            if entry is None:
+                entry = run_summary(run)
+                entry["workload"] = (f"BASELINE config {cfg}: {run['meta']['model'].upper()} PMCMC, N={run['N']}, "
+                                     f"T={run['T']}, {chains} chain(s) per GPU")
+                entry["roofline"] = roofline(run, run["value"])
+                if run["proposal"] == proposal(run["meta"], "fixed_theta")[2]:
+                    entry["proposal_kind"] = "fixed_theta (the config has no reference proposal)"
+                    break
+                entry["proposal_kind"] = "config"
+            else:
+                entry["fixed_theta"] = run_summary(run)
+        if chains == 1 and ctx.rank == 0 and ctx.world == 1:
+            entry["prefetch_auto"] = prefetch_chain(args, run["Y"], run["meta"], run["N"], run["T"], ctx.local, "auto",
+                                                    40, h=entry["h"], sigma=run["meta"]["sigma"])
+        out[name] = entry
+    return out
+
+
 def main():
     args = parse()
+    msg = resolve_gpus(args, os.environ)
+    if msg:
+        sys.exit(msg)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("EPIPF_DIST_BACKEND", "nccl")   # nccl = RCCL over xGMI; gloo only for rehearsals
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args, sys.argv[1:]))
-    if "WORLD_SIZE" in os.environ and world != args.gpus:
-        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     dist = None
     # EPIPF_BENCH_DIST=1: the distributed path (process group, max/sum reductions, RCCL all-gather) even at one rank,
     # so that a one-GPU box rehearses the RCCL code of the driver's N-GPU runs (scripts/rccl_bench_check.sh)
@@ -190,152 +477,40 @@ def main():
             assert len({tuple(d) for d in devices}) == world, f"ranks share a GPU under nccl: {devices}"
     import torch
 
-    from epipf import datasets
-    from epipf.distributed import gather_draws, pack_draws, shard
-    from epipf.engine import Engine
-    from epipf.pmcmc import ChainSampler, chain_key, run_pipelined
-
-    Y, meta = datasets.benchmark_dataset(args.config)
-    N, T = (args.particles or meta["N"]), Y.shape[0]
-    C = args.chains
-    gid = shard(C * world, world, rank)                              # global chain ids of this rank
-    pipelines = args.pipelines or (2 if N * T <= 20000 else 1)   # host-bound MH steps: overlap two samplers' host work
-    P = max(1, min(pipelines, C))
-    streams_env = max(1, min(int(os.environ.get("EPIPF_STREAMS", 4)), 8))
-    samplers = []
-    for k in range(P):                                               # contiguous chain groups, one engine each
-        ids = gid[k * C // P:(k + 1) * C // P]
-        kw = {}
-        if P > 1:
-            eng_k = Engine(meta["model"], len(np.atleast_1d(meta["n_population"])), N, T, len(ids), device=local)
-            eng_k.set_streams(max(1, streams_env // P))
-            kw["engine"] = eng_k
-        samplers.append(ChainSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=args.warmup + args.steps + 2,
-                                     observations=meta.get("observations", False), probs=meta["probs"], n_particles=N,
-                                     n_population=meta["n_population"], mu=meta["mu"],
-                                     rngs=[np.random.RandomState(args.seed + g) for g in ids],
-                                     keys=[chain_key(args.seed, g) for g in ids], device=local, mh_ratio="log", **kw))
-    engines = [s.eng for s in samplers]
-    streams = P * max(1, streams_env // P) if P > 1 else min(streams_env, C)   # concurrent step launches
-    for s_ in samplers:
-        s_.initialise()
-    run_pipelined(samplers, args.warmup) if P > 1 else [samplers[0].step() for _ in range(args.warmup)]
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    def stats_sum():
-        tot = {}
-        for e in engines:
-            for k, v in e.stats().items():
-                tot[k] = tot.get(k, 0) + v
-        return tot
-
     from epipf import _lib
-    for e in engines:
-        e.reset_stats()
-        e.set_profiling(_lib.PROFILE_TIMING)     # HIP events only: the timed kernels are the production ones
-    barrier()
-    t0 = time.perf_counter()
-    if P > 1:
-        filters = run_pipelined(samplers, args.steps)
-    else:
-        filters = sum(samplers[0].step() for _ in range(args.steps))
-    # end of run: gather every rank's posterior draws over RCCL (xGMI), SURVEY.md §8e
-    results = [r for s_ in samplers for r in s_.results()]
-    gathered = gather_draws(pack_draws(results, upto=samplers[0].i), local, force=force_dist)
-    barrier()
-    dt = time.perf_counter() - t0
-    st = stats_sum()
-    # one extra, untimed MH iteration with device counters on: SSA events/s and SIMD lane use
-    for e in engines:
-        e.reset_stats()
-        e.set_profiling(_lib.PROFILE_COUNTERS)
-    run_pipelined(samplers, 1) if P > 1 else samplers[0].step()
-    for e in engines:
-        e.set_profiling(_lib.PROFILE_OFF)
-    cst = stats_sum()
+    from epipf.chains_io import gelman_rubin
+    from epipf.distributed import unpack_draws
 
-    # max over ranks of the wall time; sum of filters
-    if dist is not None:
-        tt = torch.tensor([dt, float(filters)], dtype=torch.float64,
-                          device=f"cuda:{local}" if backend == "nccl" else "cpu")
-        mx = tt.clone()
-        dist.all_reduce(mx[0:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(mx[1:2], op=dist.ReduceOp.SUM)
-        dt, filters_all = float(mx[0]), int(mx[1])
-    else:
-        filters_all = filters
-    value = filters_all * N * T / dt
-
-    # roofline of the dominant kernel: pf_step_kernel (resample + gather + SSA + weight + in-block scan)
-    # One filter step of every chain on this rank is issued as `streams` concurrent pf_step_kernel launches, one
-    # per chain group on its own stream.  The roofline is per kernel launch, as rocprofv3 sees it:
-    # HIP events on each group's stream span its back-to-back step kernels (launch-to-completion, so a kernel
-    # waiting for CUs held by the other groups counts; rocprofv3's durations do not); the step wall time too.
-    launches = max(1, st["step_kernel_launches"])
-    avg_launch_s = st["step_kernel_ms"] / 1e3 / launches
-    step_wall_s = st["step_ms"] / 1e3 / max(1, st["step_launches"])
-    units_per_launch = filters * N / args.steps / streams            # particle-steps per kernel launch
-    n_comp = {"sir": 3, "seir": 4}.get(meta["model"], 3 * len(np.atleast_1d(meta["n_population"])))
-    bytes_per_unit = 8 * n_comp + 40                                  # 8C+40 B per particle-step
-    live_gbs = units_per_launch * bytes_per_unit / avg_launch_s / 1e9
-    # chip level: algorithmic bytes of every particle-step of the timed region over its wall time
-    chip_gbs = filters * N * T * bytes_per_unit / dt / 1e9
-    traffic = traffic_raw = None
-    valu = None
-    rocprof_us = None
-    pmc_path = os.path.join(REPO, "profiles", "pmc_step_kernel.json")
-    pmc = {}
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-        except (OSError, ValueError):
-            pmc = {}
-    # SSA lanes per particle of the timed runs (1: pf_step_kernel; > 1: the lane-group kernel)
-    lanes = int(engines[0].stats()["last_lanes"]) or 1
-    # the committed PMC pass profiles the default bench (config 2, 256 chains per GPU, one lane per particle) on one
-    # build of the library: it is used only when the library timed here carries the same build id (a hash of every
-    # kernel source and flag, epipf_build_id); after any kernel change it reads as stale and the PMC fields are null
-    pmc_current = pmc.get("build_id") == _lib.build_id()
-    if pmc_current and pmc.get("config", 2) == args.config and pmc.get("chains_per_gpu", 256) == C and lanes == 1:
-        # MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE counts half the bytes of a coalesced read stream, so
-        # `traffic` doubles the read side (FETCH x 2 + WRITE); the raw counter sum is `traffic_raw`
-        per_unit = pmc.get("hbm_bytes_per_particle_step_read_doubled")
-        traffic = per_unit * units_per_launch if per_unit else None
-        raw_unit = pmc.get("hbm_bytes_per_particle_step")
-        traffic_raw = raw_unit * units_per_launch if raw_unit else None
-        rocprof_us = pmc.get("trace_avg_us")
-        # the bound: vector-instruction issue.  SQ_INSTS_VALU per particle-step of the committed PMC
-        # pass (whole-chip sum) x the live rate, against 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
-        # instruction (MI355X_MICROARCH.md); the loop's mix (half VOP3 / 64-bit multiplies at ~4 cycles) caps the
-        # reachable fraction near 0.55 of that peak
-        ins = pmc.get("pmc_avg_per_launch", {}).get("SQ_INSTS_VALU")
-        units = pmc.get("particle_steps_per_launch")
-        if ins and units:
-            per_ps = ins / units
-            valu = {"achieved": per_ps * value, "instr_per_particle_step": per_ps,
-                    "cycles_per_instr_at_2.4GHz": VALU_PEAK * 2 / (per_ps * value),
-                    # VALU pipe busy per SIMD-cycle, SQ_ACTIVE_INST_VALU / GRBM_GUI_ACTIVE of the PMC pass
-                    # (dispatches serialised there, so each carries its own launch tail)
-                    "pmc_valu_busy_frac": pmc.get("valu_busy_frac")}
-    hbm_us = rocprof_us or avg_launch_s * 1e6
-    hbm_gbs = units_per_launch * bytes_per_unit / (hbm_us / 1e6) / 1e9
-    hbm = {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
-           "duration_source": "rocprofv3 average kernel duration (profiles/pmc_step_kernel.json)" if rocprof_us
-           else "HIP events (launch to completion)",
-           "frac_hip_event_span": live_gbs / HBM_PEAK_GBS, "chip_level_frac": chip_gbs / HBM_PEAK_GBS,
-           "bytes_per_particle_step": bytes_per_unit, "traffic": traffic, "traffic_raw": traffic_raw}
+    ctx = Ctx(world, rank, local, dist, force_dist, backend)
+    C = args.chains
+    from epipf import datasets
+    Y, meta0 = datasets.benchmark_dataset(args.config)
+    N0, T0 = (args.particles or meta0["N"]), Y.shape[0]
+    pipelines = args.pipelines or (2 if N0 * T0 <= 20000 else 1)   # host-bound MH steps: overlap two samplers' host work
+    streams_env = max(1, min(int(os.environ.get("EPIPF_STREAMS", 4)), 8))
+    run = timed_chains(ctx, args, args.config, C, args.steps, args.warmup, args.proposal, pipelines, streams_env)
+    run["cfg"] = args.config
+    meta, N, T, P, st, cst = run["meta"], run["N"], run["T"], run["P"], run["st"], run["cst"]
+    value, dt = run["value"], run["dt"]
+    lanes = run["lanes"]
+    roof = roofline(run, value)
     # SSA events per second of job time: events per particle-step (counters iteration) x the measured rate
     events_per_s = value * cst["events"] / cst["particle_steps"] if cst["particle_steps"] else None
     lane_use = cst["lane_iterations"] / cst["wave_lane_slots"] if cst["wave_lane_slots"] else None
+    gathered = run["gathered"]
+    # Gelman-Rubin R-hat (helpers.py:15-43) of the gathered chains' timed draws: a bench run is tens of iterations
+    # from a fixed start, far too short for a convergence diagnostic, so it is reported, not judged
+    rhat = None
+    th_g, _ = unpack_draws(gathered, len(run["samplers"][0].thetas[0, 0]))
+    if th_g.shape[0] >= 2 and th_g.shape[1] >= 3:
+        with np.errstate(divide="ignore", invalid="ignore"):
+            rhat = [None if not np.isfinite(v) else float(v) for v in gelman_rubin(list(th_g))]
 
     single = prefetch = None
     if args.single_chain and rank == 0 and world == 1:
-        s1 = ChainSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=args.steps + 2, probs=meta["probs"],
-                          observations=meta.get("observations", False),
+        from epipf.pmcmc import ChainSampler, chain_key
+        s1 = ChainSampler(Y, meta["model"], list(meta["theta"]), run["h"], sigma=run["sigma"], iters=args.steps + 2,
+                          probs=meta["probs"], observations=meta.get("observations", False),
                           n_particles=N, n_population=meta["n_population"], mu=meta["mu"],
                           rngs=[np.random.RandomState(args.seed)], keys=[chain_key(args.seed, 0)], device=local,
                           mh_ratio="log")
@@ -346,30 +521,12 @@ def main():
         f1 = sum(s1.step() for _ in range(args.steps))
         torch.cuda.synchronize()
         single = f1 * N * T / (time.perf_counter() - t1)
-        # the same chain with prefetching (epipf.prefetch): speculative filters of future iterations share one
-        # batched launch sequence; only filters on the realised path count
-        from epipf.prefetch import PrefetchSampler
-        s2 = PrefetchSampler(Y, meta["model"], list(meta["theta"]), 1e-4, iters=args.prefetch_iters + 40,
-                             probs=meta["probs"], observations=meta.get("observations", False), n_particles=N,
-                             n_population=meta["n_population"], mu=meta["mu"],
-                             rngs=[np.random.RandomState(args.seed)], keys=[chain_key(args.seed, 0)], device=local,
-                             mh_ratio="log", slots=args.prefetch)
-        s2.initialise()
-        while s2.i < 20:
-            s2.advance()
-        torch.cuda.synchronize()
-        i0, f0, r0, sp0 = s2.i, s2.filters_run[0], s2.rounds, s2.speculative_filters
-        t2 = time.perf_counter()
-        while s2.i < i0 + args.prefetch_iters:
-            s2.advance()
-        torch.cuda.synchronize()
-        dt2 = time.perf_counter() - t2
-        prefetch = {"value": (s2.filters_run[0] - f0) * N * T / dt2, "slots": args.prefetch,
-                    "iterations": s2.i - i0, "rounds": s2.rounds - r0,
-                    "iterations_per_round": (s2.i - i0) / max(1, s2.rounds - r0),
-                    "filters_evaluated": s2.speculative_filters - sp0,
-                    "acceptance_rate": (s2.acceptances[0] - 1) / max(1, s2.filters_run[0]),
-                    "ms_per_iteration": dt2 * 1e3 / max(1, s2.i - i0)}
+        prefetch = prefetch_chain(args, Y, meta, N, T, local, args.prefetch, args.prefetch_iters, h=run["h"],
+                                  sigma=run["sigma"])
+        prefetch_auto = prefetch_chain(args, Y, meta, N, T, local, "auto", args.prefetch_iters, h=run["h"],
+                                       sigma=run["sigma"])
+
+    configs = config_runs(ctx, args)
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -398,18 +555,9 @@ def main():
                        "pipelines": P,
                        "parallelism": f"chains sharded over {n_gpus} GPU(s) ({world} rank(s)), RCCL all-gather of "
                                       f"draws at end"},
-            # pf_step_kernel is bound by vector-instruction issue (the SSA event loop), not by HBM: the primary
-            # roofline is VALU issue; the HBM figures the north star asks for are in `hbm`
-            "roofline": {"bound": "valu", "kernel": "pf_step_kernel" if lanes == 1 else f"pf_step_group_kernel (W={lanes})",
-                         "achieved": valu["achieved"] if valu else None, "peak": VALU_PEAK,
-                         "unit": "wave64 VALU instr/s", "frac": valu["achieved"] / VALU_PEAK if valu else None,
-                         "traffic": traffic, "valu_issue": valu, "hbm": hbm,
-                         "avg_launch_us": avg_launch_s * 1e6, "particle_steps_per_launch": units_per_launch,
-                         "concurrent_launches_per_step": streams, "step_wall_us": step_wall_s * 1e6,
-                         # the same kernel's average dispatch duration in the committed rocprofv3 trace of this
-                         # command (profiles/pmc_step_kernel.json); the HIP-event figure above also counts the time a
-                         # launch waits for CUs held by the concurrent chain-group launches
-                         "rocprof_avg_launch_us": rocprof_us},
+            "proposal": {"h": run["h"], "sigma": run["sigma"], "kind": args.proposal, "source": run["proposal"],
+                         "acceptance_rate": run["acceptance_rate"]},
+            "roofline": roof,
             "events_per_s": events_per_s,
             "ssa_lane_utilisation": lane_use if lanes == 1 else None,
             "lanes_per_particle": lanes,
@@ -420,21 +568,24 @@ def main():
             "resample_ref_ambiguous": cst["resample_ref_ambiguous"],
             "resample_draws": cst["particle_steps"] * (T - 1) // T,
             "library_build_id": _lib.build_id(),
-            "pmc_profile": {"build_id": pmc.get("build_id"), "current": pmc_current},
+            "pmc_profile": {"build_id": roof["pmc_profile"]["build_id"], "path": roof["pmc_profile"]["path"],
+                            "current": roof["pmc_profile"]["path"] is not None},
             "events_per_particle_step": cst["events"] / cst["particle_steps"] if cst["particle_steps"] else None,
             # particle-steps the certified f32 SSA path handed to the exact loop, and waves that waited on one
             "ssa_exact_particle_frac": cst["ssa_exact_lanes"] / cst["particle_steps"] if cst["particle_steps"] else None,
             "ssa_exact_wave_frac": cst["ssa_exact_waves"] * 64 / cst["particle_steps"] if cst["particle_steps"] else None,
-            # every rank's posterior draws after the RCCL all-gather (R-hat is not reported: a bench run is tens of
-            # iterations from a fixed start, far too short for a convergence diagnostic)
+            # every rank's posterior draws after the RCCL all-gather, and their Gelman-Rubin R-hat per parameter
             "gathered_draws_shape": list(gathered.shape),
+            "gathered_rhat": rhat,
             "rank_devices": [f"{h}:{d}" for h, d in devices],
+            "configs": configs,
             "cpu_baseline": base,
         }
         if single is not None:
             line["single_chain_value"] = single
         if prefetch is not None:
             line["single_chain_prefetch"] = prefetch
+            line["single_chain_prefetch_auto"] = prefetch_auto
         if base is not None:
             line["speedup_vs_cpu_baseline"] = value / base["value"]
             line["speedup_vs_cpu_single_core"] = value / base["single_core"]["value"]

@@ -126,7 +126,8 @@ int epipf_run(epipf_ctx* ctx, int n_chains, const double* theta, int d, int obs_
 int epipf_copy_history(epipf_ctx* ctx, int n_chains, int32_t* hidden_out, int32_t* ancestry_out);
 
 /* On-device particle_path_sampler (pmcmc.py:236-248, including its ancestry[p] indexing) for each chain of
- * the last run; chosen [n_chains] is the host's np.random.randint(0, N) draw.  traj_out [n_chains*T*C]. */
+ * the last run; chosen [n_chains] is the host's np.random.randint(0, N) draw.  traj_out [n_chains*T*C].
+ * A chain whose last run was not EPIPF_STATUS_OK (degenerate or skipped) gets zeros: its history is not walked. */
 int epipf_path_sample(epipf_ctx* ctx, int n_chains, const int32_t* chosen, int32_t* traj_out);
 
 /* Batched last-value SSA from n states [n*C] over [0, max_time] (gillespie_algo.py *_simulate with

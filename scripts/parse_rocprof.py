@@ -1,6 +1,7 @@
 """Summarise a scripts/profile.sh session: per-kernel stats of the trace pass and per-launch PMC averages
-of pf_step_kernel.  Writes <dir>/pmc_step_kernel.json (copied to profiles/ when committed; bench.py reads
-profiles/pmc_step_kernel.json for roofline.traffic).
+of the profiled kernel (PMC_KERNEL: pf_step_kernel, or pf_step_group_kernel with PMC_LANES lanes per particle).
+Writes <dir>/<PMC_NAME> (default pmc_step_kernel.json; copied to profiles/ when committed: bench.py picks the
+profiles/pmc_*.json whose build id, config, chains per GPU and lanes match the run it reports).
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE
 counts 64 B per 128-B request of a wide coalesced stream (read side up to 2x low).  We report the raw
@@ -25,23 +26,23 @@ def main(d):
         for r in rows(p):
             print(f"  {r['Name'][:90]:90s} calls={r['Calls']:>6s} avg_us={float(r['AverageNs'])/1e3:10.2f} "
                   f"total_ms={float(r['TotalDurationNs'])/1e6:9.2f} pct={float(r['Percentage']):6.2f}")
-            if "pf_step_kernel" in r["Name"]:
+            if KERNEL in r["Name"]:
                 out["trace_avg_us"] = float(r["AverageNs"]) / 1e3
                 out["trace_calls"] = int(r["Calls"])
                 out["kernel"] = r["Name"]
     for p in glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursive=True):
-        ks = sorted((r for r in rows(p) if "pf_step_kernel" in r["Kernel_Name"]), key=lambda r: int(r["Start_Timestamp"]))
+        ks = sorted((r for r in rows(p) if KERNEL in r["Kernel_Name"]), key=lambda r: int(r["Start_Timestamp"]))
         durs = sorted((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in ks)
         if durs:
             n = len(durs)
-            print(f"# pf_step_kernel durations (us) over {n} launches: min {durs[0]:.1f} p50 {durs[n // 2]:.1f} "
+            print(f"# {KERNEL} durations (us) over {n} launches: min {durs[0]:.1f} p50 {durs[n // 2]:.1f} "
                   f"p90 {durs[int(n * .9)]:.1f} p99 {durs[int(n * .99)]:.1f} max {durs[-1]:.1f} "
                   f"sum {sum(durs) / 1e3:.1f} ms; launches > 5x median: {sum(x > 5 * durs[n // 2] for x in durs)}")
     per = defaultdict(lambda: defaultdict(float))   # counter -> dispatch -> value
     meta = {}
     for p in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
         for r in rows(p):
-            if "pf_step_kernel" not in r["Kernel_Name"]:
+            if KERNEL not in r["Kernel_Name"]:
                 continue
             per[r["Counter_Name"]][(p, r["Dispatch_Id"])] += float(r["Counter_Value"])
             meta = {k: r.get(k) for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "VGPR_Count",
@@ -54,9 +55,9 @@ def main(d):
         raw = (avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024.0
         out["hbm_bytes_per_launch"] = raw
         out["hbm_bytes_per_launch_read_doubled"] = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024.0
-        # per particle-step (one lane per particle): launches of chain groups on concurrent streams have
+        # per particle-step (LANES lanes per particle): launches of chain groups on concurrent streams have
         # different grid sizes than a one-launch-per-step run, so bench.py scales this figure instead
-        lanes = float(meta.get("Grid_Size") or 0)
+        lanes = float(meta.get("Grid_Size") or 0) / LANES
         if lanes > 0:
             out["hbm_bytes_per_particle_step"] = raw / lanes
             out["hbm_bytes_per_particle_step_read_doubled"] = out["hbm_bytes_per_launch_read_doubled"] / lanes
@@ -67,8 +68,8 @@ def main(d):
     both = [k for k in act if k in gui]
     if both:
         out["valu_busy_frac"] = 4.0 * sum(act[k] for k in both) / (1024.0 * sum(gui[k] for k in both) / 8.0)
-    lanes = float(meta.get("Grid_Size") or 0)
-    if lanes > 0:   # one lane per particle (padding of the last block included: < 0.5% at N = 10^4)
+    lanes = float(meta.get("Grid_Size") or 0) / LANES
+    if lanes > 0:   # LANES lanes per particle (padding of the last block included: < 0.5% at N = 10^4)
         out["particle_steps_per_launch"] = lanes
     # the library build these counters belong to (bench.py uses them only for the same build id)
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -76,13 +77,17 @@ def main(d):
     from epipf import _lib
     out["build_id"] = _lib.build_id()
     out.update({k: v for k, v in (("config", CONFIG), ("chains_per_gpu", CHAINS)) if v is not None})
+    out["lanes"] = LANES
     print(json.dumps(out, indent=1))
-    with open(os.path.join(d, "pmc_step_kernel.json"), "w") as f:
+    with open(os.path.join(d, NAME), "w") as f:
         json.dump(out, f, indent=1)
 
 
 CONFIG = int(os.environ["PMC_CONFIG"]) if os.environ.get("PMC_CONFIG") else None        # bench --config profiled
 CHAINS = int(os.environ["PMC_CHAINS"]) if os.environ.get("PMC_CHAINS") else None        # bench --chains profiled
+KERNEL = os.environ.get("PMC_KERNEL", "pf_step_kernel")                                  # kernel name profiled
+LANES = int(os.environ.get("PMC_LANES", "1"))                                            # its lanes per particle
+NAME = os.environ.get("PMC_NAME", "pmc_step_kernel.json")
 
 if __name__ == "__main__":
     main(sys.argv[1])

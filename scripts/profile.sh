@@ -8,7 +8,8 @@ export TMPDIR=/tmp
 TAG=${TAG:-r1}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-BENCH="bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-single-chain ${BENCH_ARGS:-}"
+BENCH="bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-single-chain --configs none ${BENCH_ARGS:-}"
+K=${PMC_KERNEL:-pf_step_kernel}
 step() {  # step <name> <timeout> <cmd...>
     local name=$1 t=$2; shift 2
     echo "== $name ($(date +%T))"
@@ -18,9 +19,9 @@ step() {  # step <name> <timeout> <cmd...>
     if [ $rc -ne 0 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
 }
 step trace 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $BENCH
-step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex pf_step_kernel -d $OUT/fetch -o run --output-format csv -- python3 $BENCH
-step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex pf_step_kernel -d $OUT/write -o run --output-format csv -- python3 $BENCH
-step pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-include-regex pf_step_kernel -d $OUT/sq -o run --output-format csv -- python3 $BENCH
-step pmc_valu 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --kernel-include-regex pf_step_kernel -d $OUT/valu -o run --output-format csv -- python3 $BENCH
+step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex $K -d $OUT/fetch -o run --output-format csv -- python3 $BENCH
+step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex $K -d $OUT/write -o run --output-format csv -- python3 $BENCH
+step pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-include-regex $K -d $OUT/sq -o run --output-format csv -- python3 $BENCH
+step pmc_valu 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --kernel-include-regex $K -d $OUT/valu -o run --output-format csv -- python3 $BENCH
 python3 scripts/parse_rocprof.py $OUT > $OUT/summary.txt 2>&1; cat $OUT/summary.txt
 echo "== done"

@@ -135,6 +135,11 @@ __global__ __launch_bounds__(256, 8) void abc_trials_kernel(AbcArgs a) {   // 8 
 // one trial (epipf_group.hpp's group_propagate, the filter's lane-group SSA: bit-identical to the exact loop), the
 // day rows written by the lane that holds the state before each day-crossing event.  Concurrent with the one-lane
 // kernel over the rest (its own stream), which fills the SIMDs the groups leave idle.
+// Early rejection on lane groups (round 4): each lane sums the distance terms of the day rows it writes
+// (the rows of the events it owns); after every chunk the group adds its lanes' sums and stops once the total exceeds
+// reject_sum -- the same proof as abc_exact_path's (any order of summing the non-negative terms fl(|x - y|) stays
+// within (1 + u)^(2T + 2) of the exact sum), so a trial stopped here is rejected, and stopping one chunk later than
+// the one-lane walk changes nothing the distance kernel reads (a rejected trial's table is never read).
 struct AbcDays {
     static constexpr bool kOn = true;
     int32_t* col;
@@ -143,6 +148,8 @@ struct AbcDays {
     double next_day;
     bool lead;                                  // group lane 0: writes on the exact path and the tail rows
     const AbcArgs* a;
+    double acc = 0.0;                           // this lane's distance terms (rows it wrote)
+    bool rejected = false;                      // group-uniform
     // event at clock tt (<= T-1): the rows of the days before it hold the state before the event (owner: this lane)
     template <class F>
     __device__ __forceinline__ void passed(double tt, bool owner, const F& before, const double* x0) {
@@ -151,17 +158,26 @@ struct AbcDays {
                 double xs[3] = {x0[0], x0[1], x0[2]};
                 before.save(xs);
                 write_day(col, n, day, xs[0], xs[1], xs[2]);
+                acc += fabs(xs[1] - a->Y[3 * day + 1]) + fabs(xs[2] - a->Y[3 * day + 2]);   // abc_algo.py:12
             }
             ++day;
             next_day += 1.0;
         }
     }
-    // outside the f32 test's range: the one-lane kernel's exact loop, rows by the lead lane
+    // after a chunk: the group's total against reject_sum (every lane of the group gets the same answer)
+    template <int W>
+    __device__ __forceinline__ bool reject_now() {
+        double tot = acc;
+#pragma unroll
+        for (int o = W / 2; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+        rejected = tot > a->reject_sum;
+        return rejected;
+    }
+    // outside the f32 test's range: the one-lane kernel's exact loop (with its early rejection), rows by the lead lane
     __device__ __forceinline__ int exact(double* x, const ChainParam& cp, uint32_t t, uint32_t, double,
                                          const LogTab* __restrict__ tab) {
         int iters = 0;
-        bool rejected;
-        return abc_exact_path(x, cp, t, *a, tab, col, lead, day, next_day, iters, INFINITY, rejected);
+        return abc_exact_path(x, cp, t, *a, tab, col, lead, day, next_day, iters, a->reject_sum, rejected);
     }
 };
 
@@ -190,7 +206,8 @@ __global__ __launch_bounds__(256) void abc_trials_group_kernel(AbcArgs a) {
         double xf[3];
         nev = group_propagate<kSIR, 1, W, 1, AbcDays>(x, xf, cp, t, kDomainAbcSsa, a.last_day, tab, &d);
         if (gl == 0) {
-            for (; d.day < a.T; ++d.day) write_day(d.col, n, d.day, xf[0], xf[1], xf[2]);
+            if (d.rejected) d.col[0] = -1;                         // row 0's S: abc_distance_kernel's marker
+            else for (; d.day < a.T; ++d.day) write_day(d.col, n, d.day, xf[0], xf[1], xf[2]);
             a.theta[i] = cp.theta[0];
             a.theta[n + i] = cp.theta[1];
         } else {

@@ -517,7 +517,7 @@ int epipf_path_sample(epipf_ctx* c, int n_chains, const int32_t* chosen, int32_t
     PathArgs a{};
     a.n_chains = n_chains; a.N = c->N; a.T = c->last_T; a.C = c->C;
     a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride;
-    a.hidden = c->hidden; a.ancestry = c->ancestry; a.chosen = c->chosen; a.traj = c->traj;
+    a.hidden = c->hidden; a.ancestry = c->ancestry; a.chosen = c->chosen; a.status = c->status; a.traj = c->traj;
     hipError_t le = launch_path_sample(a, c->stream);
     if (le != hipSuccess) return fail(EPIPF_EHIP, "path kernel launch failed: %s", hipGetErrorString(le));
     HIP_TRY(hipMemcpyAsync(traj_out, c->traj, sizeof(int32_t) * (size_t)n_chains * a.T * a.C, hipMemcpyDeviceToHost, c->stream));

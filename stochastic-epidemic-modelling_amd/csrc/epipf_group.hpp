@@ -380,6 +380,12 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
             ph[0] += tB - tA; ph[1] += tC - tB; ph[2] += tD - tC; ph[3] += tE - tD; ph[4] += tF - tE; ph[5] += 1;
         }
 #endif
+        if constexpr (Days::kOn) {                       // ABC early rejection, once per chunk (group-uniform)
+            if (days->template reject_now<W>()) {
+                put(st, 0);
+                return nev + E;
+            }
+        }
         const int stop = inside < nk ? inside : -1;
         t = tt;
         if (stop >= 0 || nk < E) {                       // the step ends before event `end` (past tmax or extinct)

@@ -71,6 +71,7 @@ struct PathArgs {
     const int32_t* hidden;
     const int32_t* ancestry;
     const int32_t* chosen;
+    const int32_t* status;      // the last run's chain status: only EPIPF_STATUS_OK chains are walked
     int32_t* traj;
 };
 

@@ -226,10 +226,14 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
 __global__ void path_sample_kernel(PathArgs a) {
     const int chain = blockIdx.x * blockDim.x + threadIdx.x;
     if (chain >= a.n_chains) return;
+    int32_t* out = a.traj + (size_t)chain * a.T * a.C;
+    if (a.status[chain] != 0) {                      // degenerate or skipped in the last run: its history rows may be
+        for (int i = 0; i < a.T * a.C; ++i) out[i] = 0;   // stale or unwritten, so it is not walked (zeros returned)
+        return;
+    }
     int chosen = checked_index(a.chosen[chain], a.N);
     const int32_t* hid = a.hidden + (size_t)chain * a.hist_stride;
     const int32_t* anc = a.ancestry + (size_t)chain * a.anc_stride;
-    int32_t* out = a.traj + (size_t)chain * a.T * a.C;
     for (int c = 0; c < a.C; ++c) out[(size_t)(a.T - 1) * a.C + c] = hid[((size_t)(a.T - 1) * a.N + chosen) * a.C + c];
     for (int p = a.T - 2; p >= 0; --p) {
         chosen = checked_index(anc[(size_t)p * a.N + chosen], a.N);       // ancestry[p], as the reference

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -29,20 +30,50 @@ void fill(int from, int to, double* hi, double* lo) {
 
 namespace epipf {
 
-// out[n] = hi and out[n_max + 1 + n] = lo of log(n!) for n = 0..n_max (lgammaq: ~2 us per entry, threaded above
-// 64k entries)
-void logfact_table(int n_max, double* out) {
-    const int n = n_max + 1;
-    double* lo = out + n;
+namespace {
+
+void fill_threaded(int from, int to, double* hi, double* lo) {
+    const int n = to - from;
     const int threads = n > 65536 ? (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1;
     if (threads == 1) {
-        fill(0, n, out, lo);
+        fill(from, to, hi, lo);
         return;
     }
     std::vector<std::thread> pool;
     for (int t = 0; t < threads; ++t)
-        pool.emplace_back(fill, (int)((long)n * t / threads), (int)((long)n * (t + 1) / threads), out, lo);
+        pool.emplace_back(fill, from + (int)((long)n * t / threads), from + (int)((long)n * (t + 1) / threads), hi, lo);
     for (auto& th : pool) th.join();
+}
+
+// Process-wide cache of the table (every entry is a function of n alone, so a table for a larger population holds
+// every smaller one as its prefix): contexts and populations share it, and a larger population only computes the
+// entries past the cached ones.  lgammaq costs ~2 us per entry, so the cache turns repeated set_population calls
+// (one per sampler / particle_filter rebinding, several contexts per process) into copies.  Tables above
+// kLogfactCacheMax entries (268 MB of host memory) are built per call and not kept.
+constexpr int kLogfactCacheMax = 1 << 24;
+std::mutex g_lf_mu;
+std::vector<double> g_lf_hi, g_lf_lo;
+
+}  // namespace
+
+// out[n] = hi and out[n_max + 1 + n] = lo of log(n!) for n = 0..n_max (lgammaq: ~2 us per entry, threaded above
+// 64k entries; cached up to kLogfactCacheMax entries)
+void logfact_table(int n_max, double* out) {
+    const int n = n_max + 1;
+    double* lo = out + n;
+    if (n > kLogfactCacheMax) {
+        fill_threaded(0, n, out, lo);
+        return;
+    }
+    std::lock_guard<std::mutex> lock(g_lf_mu);
+    const int have = (int)g_lf_hi.size();
+    if (have < n) {
+        g_lf_hi.resize(n);
+        g_lf_lo.resize(n);
+        fill_threaded(have, n, g_lf_hi.data(), g_lf_lo.data());
+    }
+    std::copy(g_lf_hi.begin(), g_lf_hi.begin() + n, out);
+    std::copy(g_lf_lo.begin(), g_lf_lo.begin() + n, lo);
 }
 
 // hi/lo of log(p) and log1p(-p) (the weight's per-chain constants)

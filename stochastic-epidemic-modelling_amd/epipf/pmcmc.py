@@ -474,7 +474,7 @@ def particle_mcmc_chains(Y, type_model, parameters, h, adaptive=False, sigma=Non
               filter_index_start=filter_index_start)
     if prefetch:
         from .prefetch import PrefetchSampler
-        sampler = PrefetchSampler(*args, slots=max(int(prefetch), len(rngs)), **kw)
+        sampler = PrefetchSampler(*args, slots="auto" if prefetch == "auto" else max(int(prefetch), len(rngs)), **kw)
     else:
         sampler = ChainSampler(*args, **kw)
     return sampler.run(progress=progress, on_iteration=on_iteration)
@@ -490,11 +490,11 @@ def particle_mcmc(Y, type_model, parameters, h, adaptive=False, sigma=None, n_ch
     acceptance expression verbatim (linear likelihoods, MVN factors); "log" uses log-likelihoods and
     stays correct when the likelihood underflows (T ≳ 150 observations).  prefetch=K evaluates up to K
     speculative MH iterations per batched GPU launch (epipf.prefetch; identical results, and the global
-    RandomState ends where the sequential loop leaves it); "auto" sizes K to the particle count
-    (prefetch_slots); prefetch=0 runs one filter per iteration."""
+    RandomState ends where the sequential loop leaves it); "auto" sizes each round from the chain's acceptance
+    rate and the measured round time (epipf.prefetch.SlotTuner); prefetch=0 runs one filter per iteration."""
     k = _STREAM.key if key is None else key
-    if prefetch == "auto":
-        prefetch = prefetch_slots(n_particles)
+    # "auto": speculative MH whose round width follows the chain's acceptance rate and the measured round time
+    # (epipf.prefetch.SlotTuner), within [1, 2 prefetch_slots(n_particles)]
     res = particle_mcmc_chains(Y, type_model, parameters, h, adaptive, sigma, n_chains, observations, probs,
                                n_particles, n_population, mu, rngs=[np.random], keys=[k], device=device,
                                mh_ratio=mh_ratio, resample=resample, progress=progress,

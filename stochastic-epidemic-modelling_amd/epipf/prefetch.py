@@ -117,11 +117,77 @@ def _value(src):
     return np.exp(lz[-1]), lz[-1], src.result[2]
 
 
+def expected_iterations(slots, alphas):
+    """Expected MH iterations one round commits when `slots` filters are scheduled best-first over chains whose
+    accept probability is `alphas` (the scheduler of PrefetchSampler._schedule on the ideal tree: every node a
+    filter, path probability = product of a / 1 - a along it; a round commits the realised path's evaluated
+    prefix, so the expectation is the sum of the scheduled nodes' path probabilities)."""
+    heap = [(-1.0, c) for c in range(len(alphas))]
+    heapq.heapify(heap)
+    e = 0.0
+    for _ in range(int(slots)):
+        if not heap:
+            break
+        negp, c = heapq.heappop(heap)
+        e -= negp
+        a = alphas[c]
+        heapq.heappush(heap, (negp * a, c))
+        heapq.heappush(heap, (negp * (1.0 - a), c))
+    return e
+
+
+class SlotTuner:
+    """slots="auto": the round width that maximises committed iterations per second of wall time.  A round's
+    wall time T(K) grows with its K filters once they no longer fit the idle SIMDs (the lane-group kernel and
+    the chip's fill set where), and its yield E(K) (expected_iterations) grows sub-linearly at a rate set by the
+    acceptance rate, so the best K depends on both; T(K) is measured on the chain's own rounds (each candidate
+    power of two tried twice first, then the best and its neighbours re-measured every `refresh` rounds), E(K)
+    comes from the chains' running acceptance rates."""
+
+    def __init__(self, lo, hi, tries=2, refresh=24):
+        self.cands = sorted({lo} | {k for k in (1, 2, 4, 8, 16, 32, 64, 128) if lo <= k <= hi} | {hi})
+        self.time = {}                                      # K -> EMA of round seconds
+        self.count = {k: 0 for k in self.cands}
+        self.tries, self.refresh = tries, refresh
+        self.rounds = 0
+        self.best = None
+
+    def pick(self, alphas):
+        for k in self.cands:                                # exploration: every candidate measured `tries` times
+            if self.count[k] < self.tries:
+                return k
+        rate = {k: expected_iterations(k, alphas) / self.time[k] for k in self.cands}
+        self.best = max(self.cands, key=lambda k: rate[k])
+        if self.rounds % self.refresh == 0:                 # keep the neighbours' times current
+            i = self.cands.index(self.best)
+            for j in (i - 1, i + 1):
+                if 0 <= j < len(self.cands) and self.count[self.cands[j]] < self.tries + self.rounds // self.refresh:
+                    return self.cands[j]
+        return self.best
+
+    def record(self, k, seconds):
+        self.rounds += 1
+        if k not in self.count:
+            return
+        self.count[k] += 1
+        old = self.time.get(k)
+        self.time[k] = seconds if old is None else 0.7 * old + 0.3 * seconds
+
+
 class PrefetchSampler(ChainSampler):
     """`ChainSampler` (same arguments, same results) that evaluates up to `slots` speculative MH iterations per
-    batched filter launch, shared best-first among its chains."""
+    batched filter launch, shared best-first among its chains.  slots="auto" sizes each round from the observed
+    acceptance rate and the measured round time (SlotTuner); results do not depend on the width."""
 
     def __init__(self, *args, slots=32, **kw):
+        n_particles = args[9] if len(args) > 9 else kw.get("n_particles", 1000)
+        n_chains = len(kw["rngs"]) if "rngs" in kw else 1
+        self.tuner = None
+        if slots == "auto":
+            from .pmcmc import prefetch_slots
+            hi = max(n_chains, min(64, 2 * prefetch_slots(n_particles)))
+            self.tuner = SlotTuner(max(1, n_chains), hi)
+            slots = hi
         self.slots = max(1, int(slots))
         kw["engine_chains"] = max(self.slots, int(kw.get("engine_chains", 0)))
         super().__init__(*args, **kw)
@@ -298,10 +364,16 @@ class PrefetchSampler(ChainSampler):
         """One round: schedule, evaluate (one batched filter of up to `slots` nodes), resolve.  Returns
         (iterations committed, filters of the realised path among them)."""
         f0 = sum(self.filters_run)
+        if self.tuner is not None:
+            import time
+            t0 = time.perf_counter()
+            self.slots = self.tuner.pick([self._alpha(c) for c in range(self.nc)])
         nodes = self._schedule()
         if nodes:
             self._evaluate(nodes)
         done = self._resolve()
+        if self.tuner is not None and nodes:
+            self.tuner.record(self.slots, time.perf_counter() - t0)
         self.i = min(r.i for r in self.roots)
         if self.i >= self.iters:
             self._finish()

@@ -117,3 +117,49 @@ def test_prefetch_advances_several_iterations_per_round(datasets_golden):
     s, res, _ = _run(pf.PrefetchSampler, 7, 1, **kw, slots=16)
     assert s.rounds * 2 < 60, s.rounds
     assert s.speculative_filters >= res[0].filters_run
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+def test_prefetch_auto_equals_sequential(datasets_golden, case):
+    """slots="auto" (SlotTuner: the width changes from round to round while it explores and re-measures) commits
+    exactly the sequential loop's values."""
+    Y = datasets_golden["sir_binom"]
+    kw = dict(Y=Y, type_model="sir", n_chains=60, n_population=4820, mu=20, **CASES[case])
+    seq = _run(pm.ChainSampler, 13, 1, **dict(kw))
+    pre = _run(pf.PrefetchSampler, 13, 1, **dict(kw), slots="auto")
+    _assert_same(seq, pre)
+    assert len({k for k, n in pre[0].tuner.count.items() if n}) > 1      # several widths were used
+
+
+def test_particle_mcmc_auto_prefetch_reproduces_reference_trace(pmcmc_golden):
+    """The drop-in's default (prefetch="auto") against the unmodified reference's trace."""
+    rec = pmcmc_golden["pmcmc_sir_p"]
+    pm.seed_stream(int(rec["key"]), 0)
+    np.random.seed(int(rec["seed"]))
+    kw = _golden_kwargs(rec)
+    th, lk, tr = pm.particle_mcmc(kw.pop("Y"), kw.pop("type_model"), kw.pop("parameters"), kw.pop("h"), **kw,
+                                  progress=False)
+    np.testing.assert_array_equal(th, rec["thetas"])
+    np.testing.assert_array_equal(tr, rec["trajs"])
+    np.testing.assert_allclose(lk, rec["likelihoods"], rtol=1e-9)
+
+
+def test_expected_iterations_model():
+    """E(K) of best-first scheduling: one slot commits one iteration; with acceptance a the second-best node is the
+    likelier child; with certain rejection K slots commit K iterations; several chains share the slots."""
+    assert pf.expected_iterations(1, [0.3]) == pytest.approx(1.0)
+    assert pf.expected_iterations(2, [0.3]) == pytest.approx(1.7)
+    assert pf.expected_iterations(2, [0.6]) == pytest.approx(1.6)
+    assert pf.expected_iterations(5, [0.0]) == pytest.approx(5.0)
+    assert pf.expected_iterations(3, [0.5, 0.5]) == pytest.approx(2.5)
+
+
+def test_slot_tuner_picks_the_best_measured_rate():
+    """After exploring every candidate twice, the tuner takes the width with the most expected iterations per second:
+    with round times flat up to 4 slots and linear beyond, 4 wins at acceptance 0.5."""
+    t = pf.SlotTuner(1, 16)
+    cost = {1: 1.0, 2: 1.0, 4: 1.0, 8: 2.0, 16: 4.0}
+    for _ in range(40):
+        k = t.pick([0.5])
+        t.record(k, cost[k])
+    assert t.best == 4
