@@ -388,13 +388,13 @@ def prefetch_chain(args, Y, meta, N, T, local, slots, iters, h=1e-4, sigma=None)
     import torch
     from epipf.pmcmc import chain_key
     from epipf.prefetch import PrefetchSampler
-    s2 = PrefetchSampler(Y, meta["model"], list(meta["theta"]), h, sigma=sigma, iters=iters + 40, probs=meta["probs"],
+    s2 = PrefetchSampler(Y, meta["model"], list(meta["theta"]), h, sigma=sigma, iters=iters + 200, probs=meta["probs"],
                          observations=meta.get("observations", False), n_particles=N,
                          n_population=meta["n_population"], mu=meta["mu"],
                          rngs=[np.random.RandomState(args.seed)], keys=[chain_key(args.seed, 0)], device=local,
                          mh_ratio="log", slots=slots)
     s2.initialise()
-    while s2.i < 20:
+    while s2.i < 20 or not s2.tuned:                 # slots="auto": warm up until every width has been measured
         s2.advance()
     torch.cuda.synchronize()
     i0, f0, r0, sp0, a0 = s2.i, s2.filters_run[0], s2.rounds, s2.speculative_filters, s2.acceptances[0]

@@ -118,11 +118,14 @@ struct epipf_ctx {
 // runs each particle-step 1.6-2.1x faster (1-8 chains, BASELINE configs 2 and 5: profiles/r2e_lanes_sweep*.jsonl;
 // W = 2, 16 and K > 1 measured no better).  Up to 640 blocks (4 chains of 10^4) W = 8 is faster since round 3's
 // mask-based decision pass and swizzle broadcasts (one chain: configs 2 / 3 / 5 +10% / +8% / +9%, four chains
-// +3% / 0% / +9%; at 8 chains W = 4 leads by 16-29%: profiles/r3k_lanes_sweep_chains.jsonl).
+// +3% / 0% / +9%; at 8 chains W = 4 leads by 16-29%: profiles/r3k_lanes_sweep_chains.jsonl).  Since round 4's
+// fixed-point decision pass (a chunk's decisions cost ~2.3 evaluations instead of W dependent ones) W = 16 leads at one
+// chain of 10^4 (157 blocks): configs 2 / 3 / 5 +6% / +8% / +3% over W = 8 (profiles/r4f_*), and W = 8 from two chains.
 static int pick_lanes(const epipf_ctx* c, int n_chains) {
     if (c->lanes > 0) return c->lanes;
     const long blocks = (long)n_chains * c->B;
-    return blocks <= (long)c->lane_blocks / 2 ? 8 : blocks <= (long)c->lane_blocks ? 4 : 1;
+    return blocks <= (long)c->lane_blocks / 8 ? 16 : blocks <= (long)c->lane_blocks / 2 ? 8
+         : blocks <= (long)c->lane_blocks ? 4 : 1;
 }
 
 static int pick_lane_events(const epipf_ctx* c, int W) {

@@ -688,7 +688,8 @@ struct FastSubgroupsPacked {                                           // gilles
     f2 S2[P], I2[P];
     f2 bN2[G][P];                                                      // beta[q][q2] / sum(N)
     float Ng[G], S0sum, R0sum;
-    const float* b;                                                    // beta[G][G] then gamma, f32 (SGPRs)
+    float gam;                                                         // gamma, f32 (a value: a pointer into cp would
+                                                                       // pin the whole ChainParam to scratch)
     // packed multiply (the selector scalarises a <2 x float> product whose halves are used apart); rounds each half
     // as v_mul_f32
     static __device__ __forceinline__ f2 pk_mul(f2 a, f2 b) {
@@ -721,9 +722,10 @@ struct FastSubgroupsPacked {                                           // gilles
             S0sum += S(q);
             R0sum += (float)x[3 * q + 2];
         }
-        b = cp.thetaf;
+        const float* b = cp.thetaf;                                    // beta[G][G] then gamma, f32
 #pragma unroll
         for (int q = 0; q <= G * G; ++q) ok = ok && rate_ok(b[q]);
+        gam = b[G * G];
         // beta / sum(N) once per step (VGPR pairs, for the packed products).  Each term's error is that of
         // (beta S)(I / sum(N)): four roundings before the accumulating fma (e_as unchanged).
         const float invN = (float)(1.0 / sumN);
@@ -755,7 +757,7 @@ struct FastSubgroupsPacked {                                           // gilles
                     }
                 }
             }
-            run = fmaf(b[G * G], I(q), run);
+            run = fmaf(gam, I(q), run);
             if (q * (G + 1) + G < NCH - 1) c[q * (G + 1) + G] = run;
         }
         return run;

@@ -193,16 +193,25 @@ __device__ __forceinline__ void decide_fixed_point(F& st, F* mine, const float* 
     st.advance(st, total);
 }
 
-// 1/sum(a) of the exact state (the reference's expressions, SsaState::rates)
-template <int MODEL, int G>
-__device__ __forceinline__ double exact_scale(const SsaState<MODEL, G>& ex, const ChainParam& cp) {
+// 1/sum(a) of the state s (the reference's expressions, SsaState::rates), evaluated on the exact loop's state built
+// from s's counts.  The total population N (sum(N) for the subgroups, :35 / :104 / :176) is the particle-step's
+// constant the f32 state carries: (S + I) + R of any later state is the same integer, so the value is the one
+// SsaState::load would compute, without re-adding the counts per event.  rates() reads no R.
+template <int MODEL, int G, class F>
+__device__ __forceinline__ double exact_scale(const F& s, const ChainParam& cp) {
+    SsaState<MODEL, G> ex;
     if constexpr (MODEL == kSIR) {
+        ex.S = (double)s.S; ex.I = (double)s.I; ex.N = s.N;
         double a0;
         return ex.rates(cp, a0);
     } else if constexpr (MODEL == kSEIR) {
+        ex.S = (double)s.S; ex.E = (double)s.E; ex.I = (double)s.I; ex.N = s.N;
         double a0, a01;
         return ex.rates(cp, a0, a01);
     } else {
+#pragma unroll
+        for (int g = 0; g < G; ++g) { ex.S[g] = (double)s.S(g); ex.I[g] = (double)s.I(g); }
+        ex.sumN = s.sumN;
         double cum[SsaState<MODEL, G>::NCH];
         return ex.rates(cp, cum);
     }
@@ -284,9 +293,14 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         Block r[K];
         float ulo[K];
         double L[K];
+        // the Philox key opaque per chunk: its ten round keys are then formed by scalar adds here instead of being
+        // hoisted out of the loop into 20 SGPRs, which the compiler spilled to VGPR lanes (v_readlane per round).
+        // The key is wave-uniform for every caller (one chain per block; one key per ABC run).
+        uint32_t key0 = __builtin_amdgcn_readfirstlane(cp.k0), key1 = __builtin_amdgcn_readfirstlane(cp.k1);
+        asm volatile("" : "+s"(key0), "+s"(key1));
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            r[k] = philox(base + (uint32_t)(k * W + gl), j, ptag, cp.f, cp.k0, cp.k1);
+            r[k] = philox(base + (uint32_t)(k * W + gl), j, ptag, cp.f, key0, key1);
             const float uc = __uint_as_float(0x3F800000u | (r[k].w >> 9)) - (1.0f - kUlpF);   // uf + 2^-24
             ulo[k] = uc - kB;
             L[k] = neg_log_one_minus_u01<true>(r[k].x, r[k].y, tab);                     // -log(1 - U), :62
@@ -342,37 +356,52 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             tau[k] = 0.0;
-            if (k * W + gl < nk) {
-                double xk[C];
-#pragma unroll
-                for (int c = 0; c < C; ++c) xk[c] = x0[c];
-                mine[k].save(xk);
-                SsaState<MODEL, G> ex;
-                ex.load(xk, cp);
-                tau[k] = exact_scale<MODEL, G>(ex, cp) * L[k];
-            }
+            if (k * W + gl < nk) tau[k] = exact_scale<MODEL, G>(mine[k], cp) * L[k];
         }
         // t + tau in event order (the exact loop's additions); the step ends at the first t + tau > tmax.  Branch-free:
         // the sum runs on through the chunk (events past nk add tau = 0) and `inside` counts the events before the
         // first overshoot -- once an event overshoots, t is no longer needed (the step ends in this chunk).
         double tt = t;
         int inside = 0;
-        bool alive = true;
-        auto clock = [&](auto I) __attribute__((always_inline)) -> bool {
-            constexpr int e = decltype(I)::value;
-            const uint64_t b = __double_as_longlong(tau[e / W]);
-            const uint32_t lo = group_lane_dpp<W, e % W>((uint32_t)b), hi = group_lane_dpp<W, e % W>((uint32_t)(b >> 32));
-            tt = tt + __longlong_as_double(((uint64_t)hi << 32) | lo);
-            alive = alive && !(tt > tmax);                   // :65-66
-            inside += alive ? 1 : 0;
-            if constexpr (Days::kOn) {                       // event e happened at tt: days before it (rare)
-                if (alive && e < nk) days->passed(tt, gl == e % W, mine[e / W], x0);
-            }
-            return true;
-        };
         __builtin_amdgcn_sched_barrier(0);
         EPIPF_PHASE_MARK(tE);
-        StaticFor<0, E>::run(clock);
+        if constexpr (Days::kOn) {
+            bool alive = true;
+            auto clock = [&](auto I) __attribute__((always_inline)) -> bool {
+                constexpr int e = decltype(I)::value;
+                tt = tt + group_lane_f64<W, e % W>(tau[e / W]);
+                alive = alive && !(tt > tmax);               // :65-66
+                inside += alive ? 1 : 0;
+                if (alive && e < nk) days->passed(tt, gl == e % W, mine[e / W], x0);   // days before event e (rare)
+                return true;
+            };
+            StaticFor<0, E>::run(clock);
+        } else {
+            // The sums t + tau are nondecreasing (tau >= 0; finite on this path: f32-eligible rates and counts), so
+            // every prefix is at most the chunk's total: when the total stays inside the step, so does every event,
+            // and only a chunk that overshoots (the step's last) counts the events before its first t + tau > tmax,
+            // adding again in the same order.
+            auto clock = [&](auto I) __attribute__((always_inline)) -> bool {
+                constexpr int e = decltype(I)::value;
+                tt = tt + group_lane_f64<W, e % W>(tau[e / W]);
+                return true;
+            };
+            StaticFor<0, E>::run(clock);
+            if (!(tt > tmax)) {
+                inside = E;
+            } else {
+                double t2 = t;
+                bool alive = true;
+                auto recount = [&](auto I) __attribute__((always_inline)) -> bool {
+                    constexpr int e = decltype(I)::value;
+                    t2 = t2 + group_lane_f64<W, e % W>(tau[e / W]);
+                    alive = alive && !(t2 > tmax);           // :65-66
+                    inside += alive ? 1 : 0;
+                    return true;
+                };
+                StaticFor<0, E>::run(recount);
+            }
+        }
         __builtin_amdgcn_sched_barrier(0);
         EPIPF_PHASE_MARK(tF);
 #ifdef EPIPF_PHASE_TIMING

@@ -140,28 +140,32 @@ class SlotTuner:
     """slots="auto": the round width that maximises committed iterations per second of wall time.  A round's
     wall time T(K) grows with its K filters once they no longer fit the idle SIMDs (the lane-group kernel and
     the chip's fill set where), and its yield E(K) (expected_iterations) grows sub-linearly at a rate set by the
-    acceptance rate, so the best K depends on both; T(K) is measured on the chain's own rounds (each candidate
-    power of two tried twice first, then the best and its neighbours re-measured every `refresh` rounds), E(K)
-    comes from the chains' running acceptance rates."""
+    acceptance rate, so the best K depends on both; T(K) is measured on the chain's own rounds -- each candidate power
+    of two run once to warm up (not timed: a first launch shape pays one-off costs) and then `tries` times, T(K) the
+    fastest of its last three rounds; the best and its neighbours re-measured every `refresh` rounds -- and E(K) comes
+    from the chains' running acceptance rates."""
 
     def __init__(self, lo, hi, tries=2, refresh=24):
         self.cands = sorted({lo} | {k for k in (1, 2, 4, 8, 16, 32, 64, 128) if lo <= k <= hi} | {hi})
-        self.time = {}                                      # K -> EMA of round seconds
-        self.count = {k: 0 for k in self.cands}
+        self.samples = {k: [] for k in self.cands}          # K -> the last round times (s)
+        self.count = {k: 0 for k in self.cands}              # rounds run at K (the first is a warm-up)
         self.tries, self.refresh = tries, refresh
         self.rounds = 0
         self.best = None
 
+    def time(self, k):
+        return min(self.samples[k][-3:])
+
     def pick(self, alphas):
         for k in self.cands:                                # exploration: every candidate measured `tries` times
-            if self.count[k] < self.tries:
+            if len(self.samples[k]) < self.tries:
                 return k
-        rate = {k: expected_iterations(k, alphas) / self.time[k] for k in self.cands}
+        rate = {k: expected_iterations(k, alphas) / self.time(k) for k in self.cands}
         self.best = max(self.cands, key=lambda k: rate[k])
         if self.rounds % self.refresh == 0:                 # keep the neighbours' times current
             i = self.cands.index(self.best)
             for j in (i - 1, i + 1):
-                if 0 <= j < len(self.cands) and self.count[self.cands[j]] < self.tries + self.rounds // self.refresh:
+                if 0 <= j < len(self.cands):
                     return self.cands[j]
         return self.best
 
@@ -170,8 +174,8 @@ class SlotTuner:
         if k not in self.count:
             return
         self.count[k] += 1
-        old = self.time.get(k)
-        self.time[k] = seconds if old is None else 0.7 * old + 0.3 * seconds
+        if self.count[k] > 1:
+            self.samples[k] = (self.samples[k] + [seconds])[-3:]
 
 
 class PrefetchSampler(ChainSampler):
@@ -382,6 +386,11 @@ class PrefetchSampler(ChainSampler):
     def _finish(self):
         for c in range(self.nc):
             self.fnext[c] = self.roots[c].fnext
+
+    @property
+    def tuned(self):
+        """slots="auto": whether the width tuner has measured every candidate (always True for a fixed width)."""
+        return self.tuner is None or self.tuner.best is not None
 
     def step(self):
         raise NotImplementedError("PrefetchSampler advances by rounds: use advance() or run()")
