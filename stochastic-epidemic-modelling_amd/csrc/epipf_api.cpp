@@ -119,12 +119,13 @@ struct epipf_ctx {
 // W = 2, 16 and K > 1 measured no better).  Up to 640 blocks (4 chains of 10^4) W = 8 is faster since round 3's
 // mask-based decision pass and swizzle broadcasts (one chain: configs 2 / 3 / 5 +10% / +8% / +9%, four chains
 // +3% / 0% / +9%; at 8 chains W = 4 leads by 16-29%: profiles/r3k_lanes_sweep_chains.jsonl).  Since round 4's
-// fixed-point decision pass (a chunk's decisions cost ~2.3 evaluations instead of W dependent ones) W = 16 leads at one
-// chain of 10^4 (157 blocks): configs 2 / 3 / 5 +6% / +8% / +3% over W = 8 (profiles/r4f_*), and W = 8 from two chains.
+// fixed-point decision pass (a chunk's decisions cost ~2.3 evaluations instead of W dependent ones) and the clock pass
+// through LDS, W = 16 leads up to two chains of 10^4 (320 blocks; one chain: configs 2 / 3 / 5 +12% / +16% / +18%
+// over W = 8, two chains +9% / +10% / +12%), W = 8 from three (profiles/r4i_*, r4k_*).
 static int pick_lanes(const epipf_ctx* c, int n_chains) {
     if (c->lanes > 0) return c->lanes;
     const long blocks = (long)n_chains * c->B;
-    return blocks <= (long)c->lane_blocks / 8 ? 16 : blocks <= (long)c->lane_blocks / 2 ? 8
+    return blocks <= (long)c->lane_blocks / 4 ? 16 : blocks <= (long)c->lane_blocks / 2 ? 8
          : blocks <= (long)c->lane_blocks ? 4 : 1;
 }
 

@@ -230,6 +230,8 @@ __device__ __forceinline__ double exact_scale(const F& s, const ChainParam& cp) 
 //   per lane: each kept state's 1/sum(a) (two IEEE divisions) times its -log(1 - U) = tau (SsaState::tau_of's
 //          expression);
 //   clock: t + tau in event order, stop at the first t + tau > tmax.
+// xch: this wave's LDS slice of K x 64 doubles, through which the clock pass reads the group's tau (one store per lane
+// and shared loads instead of two DPP / swizzle moves per event, which took the place of VALU issue slots).
 // Day recorder of the ABC trial (abc_kernels.hip): `days` is every event's clock in order, with the state before it.
 // The filter records nothing.
 // Phase timing (make phase -> lib/libepipf_phase.so, EPIPF_PHASE_TIMING): s_memtime at the phase fences of the chunk
@@ -248,7 +250,7 @@ struct NoDays {
 template <int MODEL, int G, int W, int K, class Days = NoDays>
 __device__ __forceinline__ int group_propagate(const double* x0, double* xout, const ChainParam& cp, uint32_t j,
                                                uint32_t ptag, double tmax, const LogTab* __restrict__ tab,
-                                               Days* days = nullptr, unsigned long long* ph = nullptr) {
+                                               double* xch, Days* days = nullptr, unsigned long long* ph = nullptr) {
     using F = typename GroupSsa<MODEL, G>::type;
     constexpr int C = Shape<MODEL, G>::C;
     constexpr int E = W * K;
@@ -365,11 +367,15 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         int inside = 0;
         __builtin_amdgcn_sched_barrier(0);
         EPIPF_PHASE_MARK(tE);
+#pragma unroll
+        for (int k = 0; k < K; ++k) xch[k * 64 + lane] = tau[k];
+        lds_sync<true>();                                // this wave's stores before its loads
+        const double* xg = xch + gb;                     // tau of event e: xg[(e / W) * 64 + e % W]
         if constexpr (Days::kOn) {
             bool alive = true;
             auto clock = [&](auto I) __attribute__((always_inline)) -> bool {
                 constexpr int e = decltype(I)::value;
-                tt = tt + group_lane_f64<W, e % W>(tau[e / W]);
+                tt = tt + xg[(e / W) * 64 + e % W];
                 alive = alive && !(tt > tmax);               // :65-66
                 inside += alive ? 1 : 0;
                 if (alive && e < nk) days->passed(tt, gl == e % W, mine[e / W], x0);   // days before event e (rare)
@@ -383,7 +389,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
             // adding again in the same order.
             auto clock = [&](auto I) __attribute__((always_inline)) -> bool {
                 constexpr int e = decltype(I)::value;
-                tt = tt + group_lane_f64<W, e % W>(tau[e / W]);
+                tt = tt + xg[(e / W) * 64 + e % W];
                 return true;
             };
             StaticFor<0, E>::run(clock);
@@ -394,7 +400,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
                 bool alive = true;
                 auto recount = [&](auto I) __attribute__((always_inline)) -> bool {
                     constexpr int e = decltype(I)::value;
-                    t2 = t2 + group_lane_f64<W, e % W>(tau[e / W]);
+                    t2 = t2 + xg[(e / W) * 64 + e % W];
                     alive = alive && !(t2 > tmax);           // :65-66
                     inside += alive ? 1 : 0;
                     return true;
@@ -435,8 +441,11 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
     }
 }
 
-// LDS of the lane-group step kernel: log table | red[16] | particle rows [64][C] int32 | block-sum prefix
-inline size_t group_lds_bytes_impl(int B, int C) { return step_lds_bytes(B, 64) + sizeof(int32_t) * 64 * (size_t)C; }
+// LDS of the lane-group step kernel: log table | tau exchange [W][K][64] | red[16] | particle rows [64][C] int32 |
+// block-sum prefix
+inline size_t group_lds_bytes_impl(int B, int C, int W, int K) {
+    return step_lds_bytes(B, 64) + sizeof(int32_t) * 64 * (size_t)C + sizeof(double) * 64 * (size_t)W * K;
+}
 
 template <int MODEL, int G, int OBS, int W, int K>
 __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p) {
@@ -445,7 +454,8 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
     constexpr int PPW = 64 / W;                          // particles per wave
     extern __shared__ __attribute__((aligned(16))) double smem[];
     LogTab* tab = reinterpret_cast<LogTab*>(smem);
-    double* red = smem + 2 * kLogTabEntries;             // [0]: the step's weight total, for every wave
+    double* xch = smem + 2 * kLogTabEntries;             // the clock pass's tau exchange, [W waves][K][64]
+    double* red = xch + 64 * W * K;                      // [0]: the step's weight total, for every wave
     int32_t* rows = reinterpret_cast<int32_t*>(red + 16);
     double* seg_start = red + 16 + (64 * C + 1) / 2;
     double* seg_end = seg_start + a.nseg;
@@ -532,7 +542,8 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
 #pragma unroll
         for (int c = 0; c < C; ++c) x0[c] = (double)rows[pl * C + c];
         const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
-        nev = group_propagate<MODEL, G, W, K>(x0, x, cp, (uint32_t)jg, ptag, 1.0, tab, (NoDays*)nullptr, ph);
+        nev = group_propagate<MODEL, G, W, K>(x0, x, cp, (uint32_t)jg, ptag, 1.0, tab, xch + wave * 64 * K,
+                                              (NoDays*)nullptr, ph);
     }
 #ifdef EPIPF_PHASE_TIMING
     const unsigned long long k2 = __builtin_readcyclecounter();

@@ -180,7 +180,7 @@ size_t step_lds_bytes(int B, int wg);
 using GroupStepFn = void (*)(const StepArgs& a, int p, dim3 grid, size_t lds, hipStream_t s);
 GroupStepFn group_step_launcher(int model, int G, int obs, int W, int K);
 bool group_shape_supported(int W, int K);
-size_t group_lds_bytes(int B, int C);
+size_t group_lds_bytes(int B, int C, int W, int K);
 int prefix_segment(int B);
 constexpr int kMaxSegments = 200;
 hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, const FilterStreams& fs);

@@ -184,7 +184,7 @@ def test_lane_groups_segmented_prefix(datasets_golden):
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5])
 def test_lane_groups_full_size_single_chain_vs_oracle(cfg, lanes):
     """Every BASELINE config at full size with one chain (the north star's layout for config 5), on the automatic
-    lane choice (W = 16 up to 160 particle blocks, 8 up to 640, 4 above) and on W = 4: config 2 (SIR, N = 10^4, T = 200), 3
+    lane choice (W = 16 up to 320 particle blocks, 8 up to 640, 4 above) and on W = 4: config 2 (SIR, N = 10^4, T = 200), 3
     (SEIR, normal observations), 4 (N = 5*10^4: 782 particle blocks, a segmented block-sum prefix), 5 (2-group SIR)
     -- bit-exact vs the oracle."""
     from epipf import datasets
@@ -205,7 +205,7 @@ def test_lane_groups_full_size_single_chain_vs_oracle(cfg, lanes):
     obs = bool(meta.get("observations", False))
     lz, st = eng.run(theta_vector(mid, ref_th)[0][None], [meta["probs"]], [4242], [7], observations=obs)
     blocks = (meta["N"] + 63) // 64
-    assert eng.stats()["last_lanes"] == (lanes or (16 if blocks <= 160 else 8 if blocks <= 640 else 4))
+    assert eng.stats()["last_lanes"] == (lanes or (16 if blocks <= 320 else 8 if blocks <= 640 else 4))
     hid, anc = eng.history(1)
     eng.close()
     o = oracle.particle_filter(Y, meta["model"], ref_th, obs, meta["probs"], meta["N"], meta["n_population"],
@@ -217,14 +217,14 @@ def test_lane_groups_full_size_single_chain_vs_oracle(cfg, lanes):
 
 
 def test_automatic_lane_choice():
-    """One chain of 10^4 particles gets 16 lanes, up to 4 chains 8, up to 8 chains 4; a batch that fills the chip keeps
-    one lane per particle."""
+    """Up to two chains of 10^4 particles get 16 lanes, up to 4 chains 8, up to 8 chains 4; a batch that fills the chip
+    keeps one lane per particle."""
     from epipf.engine import Engine
     Y = np.zeros((3, 3))
     eng = Engine("sir", 1, 10000, 3, 256)
     eng.set_observations(Y)
     eng.set_population(10000, 20)
-    for chains, want in [(1, 16), (2, 8), (4, 8), (5, 4), (8, 4), (9, 1), (256, 1)]:
+    for chains, want in [(1, 16), (2, 16), (3, 8), (4, 8), (5, 4), (8, 4), (9, 1), (256, 1)]:
         eng.run(np.tile([0.25, 0.1], (chains, 1)), [0.1] * chains, list(range(1, chains + 1)), [0] * chains)
         assert eng.stats()["last_lanes"] == want, (chains, eng.stats()["last_lanes"])
     eng.close()
