@@ -108,6 +108,8 @@ struct epipf_ctx {
     int lanes = 0;           // SSA lanes per particle: 0 = automatic (pick_lanes), else 1/2/4/8/16 (EPIPF_LANES)
     int lane_events = 0;     // events per lane per chunk of the lane-group kernel: 0 = automatic (EPIPF_LANE_EVENTS)
     int lane_blocks = 1280;  // automatic choice: lane groups up to this many particle blocks per launch
+    int group_block = 0;     // lane-group runs' particles per block: 0 = automatic (pick_block), 16 or 64 (EPIPF_GROUP_BLOCK)
+    long group_block_max = 0;  // automatic: 16-particle blocks up to this many per launch (EPIPF_GROUP_BLOCK_MAX)
     int xcd_map = 1;         // XCD-aware placement of the step launches' blocks (EPIPF_XCD_MAP=0: 2-D grid)
     double split_p = -1.0;   // probs of the cached hi/lo split of log p, log1p(-p) (chains usually share probs)
     double split[4] = {0, 0, 0, 0};
@@ -127,6 +129,17 @@ static int pick_lanes(const epipf_ctx* c, int n_chains) {
     const long blocks = (long)n_chains * c->B;
     return blocks <= (long)c->lane_blocks / 4 ? 16 : blocks <= (long)c->lane_blocks / 2 ? 8
          : blocks <= (long)c->lane_blocks ? 4 : 1;
+}
+
+// Particles per block of a run's weight layout (block sums, in-block prefixes): 64, one wave of the one-lane kernel, or
+// for lane-group runs of W >= 8 that leave CUs idle, kGroupBlock = 16 -- a chain of 10^4 particles is then 626
+// workgroups of 16 W / 64 waves instead of 157 of W waves, spread over all 256 CUs (at most 3 waves per SIMD at W = 16
+// instead of 4 on 157 CUs).  EPIPF_GROUP_BLOCK = 16 / 64 forces it.
+static int pick_block(const epipf_ctx* c, int n_chains, int W) {
+    if (W < 8) return c->wg;
+    if (c->group_block > 0) return c->group_block;
+    const long blocks = (long)n_chains * ((c->N + kGroupBlock - 1) / kGroupBlock);
+    return blocks <= c->group_block_max ? kGroupBlock : c->wg;
 }
 
 static int pick_lane_events(const epipf_ctx* c, int W) {
@@ -244,6 +257,11 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     }
     if (const char* e = getenv("EPIPF_LANE_BLOCKS")) c->lane_blocks = std::max(0, atoi(e));
     if (const char* e = getenv("EPIPF_LANE_EVENTS")) c->lane_events = std::max(0, atoi(e));
+    if (const char* e = getenv("EPIPF_GROUP_BLOCK")) {
+        const int b = atoi(e);
+        if (b == 0 || b == kGroupBlock || b == 64) c->group_block = b;
+    }
+    if (const char* e = getenv("EPIPF_GROUP_BLOCK_MAX")) c->group_block_max = std::max(0L, atol(e));
     if (const char* e = getenv("EPIPF_XCD_MAP")) c->xcd_map = atoi(e) != 0;
     c->B = (n_particles + c->wg - 1) / c->wg;
     if (step_lds_bytes(c->B, c->wg) > 160 * 1024) {
@@ -253,7 +271,8 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     c->hist_stride = (size_t)t_max * n_particles * c->C;
     c->anc_stride = (size_t)t_max * n_particles;
     c->wstride = (size_t)c->B * c->wg;
-    c->bstride = (size_t)c->B;
+    // block sums for the lane-group runs' 16-particle blocks too (pick_block, kGroupBlock)
+    c->bstride = std::max((size_t)c->B, (size_t)((n_particles + kGroupBlock - 1) / kGroupBlock));
     int rc = 0;
     if (hipSetDevice(device) != hipSuccess) { free_ctx(c); return fail(EPIPF_EHIP, "hipSetDevice(%d) failed", device); }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -396,18 +415,20 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     HIP_TRY(hipMemcpyAsync(c->status, c->h_status, sizeof(int32_t) * n_chains, hipMemcpyHostToDevice, c->stream));
 
     StepArgs a{};
-    a.N = c->N; a.T = c->T; a.B = c->B; a.wg = c->wg; a.max_chains = c->max_chains;
+    a.N = c->N; a.T = c->T; a.max_chains = c->max_chains;
+    a.lanes = pick_lanes(c, n_chains);
+    a.wg = pick_block(c, n_chains, a.lanes);
+    a.B = (c->N + a.wg - 1) / a.wg;
     a.resample_mode = resample_mode; a.count_events = c->profiling >= EPIPF_PROFILE_COUNTERS ? 1 : 0; a.lf_max = c->lf_max;
     a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride; a.wstride = c->wstride; a.bstride = c->bstride;
-    a.cert_k = cert_k(c->N, c->B, c->wg);
+    a.cert_k = cert_k(c->N, a.B, 64);                     // the block-sum scans run on 64 lanes whatever the layout
     // the reference-ambiguity test runs with the other device counters (bench.py's untimed counters iteration, the
     // parity tests); ref_k = 0 switches it off in the timed, production launches
     a.ref_k = a.count_events ? 2.0 * ref_pmf_envelope(obs_model, c->lf_max) * (1.0 + 0x1.0p-10) : 0.0;
     a.Y = c->Y; a.lf = c->lf; a.logtab = c->logtab; a.cp = c->cp; a.hidden = c->hidden; a.ancestry = c->ancestry;
     a.wraw = c->wraw; a.wloc = c->wloc; a.bsum = c->bsum; a.log_zeta = c->log_zeta; a.status = c->status;
-    a.seg = prefix_segment(c->B); a.nseg = (c->B + a.seg - 1) / a.seg;
+    a.seg = prefix_segment(a.B); a.nseg = (a.B + a.seg - 1) / a.seg;
     a.counters = c->counters;
-    a.lanes = pick_lanes(c, n_chains);
     a.lane_events = pick_lane_events(c, a.lanes);
     a.xcd_map = c->xcd_map;
     if (a.lanes > 1 && !group_shape_supported(a.lanes, a.lane_events))

@@ -1391,7 +1391,15 @@ __device__ __forceinline__ double ref_halfwidth(double v, double ref_k) {
 // those <= Ut); counting a monotone predicate is the binary search's answer.
 template <int WG, bool FLAT = false>
 __device__ __forceinline__ int inblock_search(double base, const double* __restrict__ L, double Ut) {
-    if constexpr (FLAT) {
+    if constexpr (FLAT && WG == 16) {                   // 16-particle blocks: one round of 15 independent loads
+        double c[15];
+#pragma unroll
+        for (int i = 0; i < 15; ++i) c[i] = L[i];
+        int o = 0;
+#pragma unroll
+        for (int i = 0; i < 15; ++i) o += (base + c[i] > Ut) ? 0 : 1;
+        return o;
+    } else if constexpr (FLAT) {
         static_assert(WG == 64, "8 x 8 sub-blocks");
         double c[7];
 #pragma unroll
@@ -1474,6 +1482,8 @@ __device__ __forceinline__ int resample_search_seg(double U, const double* seg_s
     int l;
     if (FLAT && WGB == 64) {
         l = inblock_search<64, true>(base, L, Ut);
+    } else if (FLAT && WGB == 16) {
+        l = inblock_search<16, true>(base, L, Ut);
     } else {
         l = 0;
         int h = WGB - 1;

@@ -447,11 +447,16 @@ inline size_t group_lds_bytes_impl(int B, int C, int W, int K) {
     return step_lds_bytes(B, 64) + sizeof(int32_t) * 64 * (size_t)C + sizeof(double) * 64 * (size_t)W * K;
 }
 
-template <int MODEL, int G, int OBS, int W, int K>
-__global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p) {
+// PB particles per block: 64 (the one-lane kernel's blocks), or kGroupBlock = 16 for runs that would leave CUs idle
+// (a.wg; the weight layout -- block sums, in-block prefixes -- is then one of 16-particle blocks, built by the init
+// kernel the same way).  Wave 0's first PB lanes hold the block's particles in the scan/search/gather and store/weigh
+// phases; the block is PB W / 64 waves.
+template <int MODEL, int G, int OBS, int W, int K, int PB>
+__global__ __launch_bounds__(PB * W) void pf_step_group_kernel(StepArgs a, int p) {
     using Sh = Shape<MODEL, G>;
     constexpr int C = Sh::C;
     constexpr int PPW = 64 / W;                          // particles per wave
+    static_assert(PB * W >= 64 && (PB * W) % 64 == 0, "whole waves");
     extern __shared__ __attribute__((aligned(16))) double smem[];
     LogTab* tab = reinterpret_cast<LogTab*>(smem);
     double* xch = smem + 2 * kLogTabEntries;             // the clock pass's tau exchange, [W waves][K][64]
@@ -469,7 +474,7 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
     const size_t wcur = ((size_t)cur * a.max_chains + chain) * a.wstride;
     const size_t bprev = ((size_t)prev * a.max_chains + chain) * a.bstride;
     const size_t bcur = ((size_t)cur * a.max_chains + chain) * a.bstride;
-    for (int i = (int)threadIdx.x; i < kLogTabEntries; i += 64 * W) tab[i] = a.logtab[i];
+    for (int i = (int)threadIdx.x; i < kLogTabEntries; i += PB * W) tab[i] = a.logtab[i];
 
 #ifdef EPIPF_PHASE_TIMING
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
@@ -478,7 +483,8 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
     unsigned long long* ph = nullptr;
 #endif
     if (wave == 0) {                                     // likelihood, resampling, gather: pf_step_kernel's code
-        const int j = bp.b * 64 + lane;
+        const int j = bp.b * PB + lane;
+        const bool mine = lane < PB && j < a.N;
         const double total = (a.seg == 1)
                                  ? scan_block_sums<64, true>(a.bsum + bprev, a.B, seg_start + a.B, seg_start, red)
                                  : scan_segments<true>(a.bsum + bprev, a.B, a.seg, a.nseg, seg_start, seg_end);
@@ -489,7 +495,7 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
             double U = 0.0;
             int anc = 0;
             bool certified = true, ambiguous = false;
-            if (j < a.N) {                               // pmcmc.py:188-190
+            if (mine) {                                  // pmcmc.py:188-190
                 const uint32_t rtag = ((uint32_t)p & 0xFFFFFFu) | kDomainResample;
                 if (a.resample_mode == 0) {
                     const Block r = philox(0u, (uint32_t)j, rtag, cp.f, cp.k0, cp.k1);
@@ -499,11 +505,11 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
                     U = ((double)j + u01(r.x, r.y)) / (double)a.N;
                 }
                 if (a.seg == 1)
-                    anc = resample_search<64, true>(U, seg_start + a.B, seg_start, a.B, total, a.wloc + wprev, a.N, a.cert_k,
+                    anc = resample_search<PB, true>(U, seg_start + a.B, seg_start, a.B, total, a.wloc + wprev, a.N, a.cert_k,
                                               certified, a.ref_k, ambiguous);
                 else
                     anc = resample_search_seg<true>(U, seg_start, seg_end, a.nseg, a.seg, a.bsum + bprev, a.B, total,
-                                              a.wloc + wprev, 64, a.N, a.cert_k, certified, a.ref_k, ambiguous);
+                                              a.wloc + wprev, PB, a.N, a.cert_k, certified, a.ref_k, ambiguous);
             }
             if (ambiguous) atomicAdd(counter_slot(a.counters) + 6, 1ull);
             if (__any(!certified)) {
@@ -513,7 +519,7 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
                     atomicAdd(counter_slot(a.counters) + 1, 1ull);
                 }
             }
-            if (j < a.N) {                               // :193-199
+            if (mine) {                                  // :193-199
                 anc = checked_index(anc, a.N);
                 a.ancestry[(size_t)chain * a.anc_stride + (size_t)p * a.N + j] = anc;
                 const int32_t* hp = a.hidden + (size_t)chain * a.hist_stride + ((size_t)(p - 1) * a.N + anc) * C;
@@ -534,7 +540,7 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
     // group SSA: wave w, group g runs particle w * PPW + g of the block
     const int gl = lane & (W - 1);
     const int pl = wave * PPW + lane / W;
-    const int jg = bp.b * 64 + pl;
+    const int jg = bp.b * PB + pl;
     int nev = 0;
     double x[C];
     if (jg < a.N) {                                      // group-uniform
@@ -561,9 +567,9 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
     __syncthreads();
 
     if (wave == 0) {                                     // store, weights for step p+1, in-block scan
-        const int j = bp.b * 64 + lane;
+        const int j = bp.b * PB + lane;
         double w = 0.0;
-        if (j < a.N) {
+        if (lane < PB && j < a.N) {
             double xs[C];
 #pragma unroll
             for (int c = 0; c < C; ++c) xs[c] = (double)rows[lane * C + c];
@@ -575,9 +581,11 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
         }
         if (p + 1 < a.T) {
             const double loc = block_inclusive_scan<64>(w, red);
-            a.wraw[wcur + j] = w;
-            a.wloc[wcur + j] = loc;
-            if (lane == 63) a.bsum[bcur + bp.b] = loc;
+            if (lane < PB) {
+                a.wraw[wcur + j] = w;
+                a.wloc[wcur + j] = loc;
+            }
+            if (lane == PB - 1) a.bsum[bcur + bp.b] = loc;
         }
     }
 #ifdef EPIPF_PHASE_TIMING
@@ -591,7 +599,14 @@ __global__ __launch_bounds__(64 * W) void pf_step_group_kernel(StepArgs a, int p
 // ------------------------------------------------------------------------------- launch table
 template <int MODEL, int G, int OBS, int W, int K>
 static void launch_group_t(const StepArgs& a, int p, dim3 grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((pf_step_group_kernel<MODEL, G, OBS, W, K>), grid, dim3(64 * W), lds, s, a, p);
+    if constexpr (W >= 8) {                              // 16-particle blocks (a.wg, pick_block): W >= 8 only
+        if (a.wg == kGroupBlock) {
+            hipLaunchKernelGGL((pf_step_group_kernel<MODEL, G, OBS, W, K, kGroupBlock>), grid, dim3(kGroupBlock * W), lds,
+                               s, a, p);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((pf_step_group_kernel<MODEL, G, OBS, W, K, 64>), grid, dim3(64 * W), lds, s, a, p);
 }
 
 // (lanes per particle W, events per lane per chunk K) instantiated

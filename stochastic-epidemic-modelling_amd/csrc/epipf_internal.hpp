@@ -37,7 +37,8 @@ __device__ __forceinline__ unsigned long long* counter_slot(unsigned long long* 
 //   log_zeta f64   [max_chains][T]
 //   Y        f64   [T][K];  lf f64 [2][lf_max+1] = log n! as hi, then lo (binary128 on the host, logfact.cpp)
 struct StepArgs {
-    int N, T, B, wg, max_chains, resample_mode, count_events, lf_max;
+    int N, T, B, wg, max_chains, resample_mode, count_events, lf_max;   // wg: particles per block of the weight
+                                                                        // layout (64; kGroupBlock for some lane runs)
     int chain0;                   // first chain of this launch (chain groups run on separate streams)
     int lanes;                    // lanes per particle in the SSA: 1 = pf_step_kernel, 2..16 = pf_step_group_kernel
     int lane_events;              // pf_step_group_kernel: events per lane per chunk
@@ -183,6 +184,7 @@ bool group_shape_supported(int W, int K);
 size_t group_lds_bytes(int B, int C, int W, int K);
 int prefix_segment(int B);
 constexpr int kMaxSegments = 200;
+constexpr int kGroupBlock = 16;   // particles per block of the lane-group runs that spread a chain over every CU
 hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, const FilterStreams& fs);
 hipError_t launch_path_sample(const PathArgs& a, hipStream_t s);
 hipError_t launch_simulate(const SimArgs& a, int model, int G, hipStream_t s);

@@ -32,13 +32,16 @@ __global__ __launch_bounds__(WG) void pf_init_kernel(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const BlockPos bp = step_block(a);
     const int chain = bp.chain;
-    const int j = bp.b * WG + threadIdx.x;
+    // a.wg particles per block: WG (one lane each), or fewer for the lane-group runs' smaller blocks (the lanes past
+    // a.wg hold no particle and weigh 0 in the scan)
+    const bool mine = (int)threadIdx.x < a.wg;
+    const int j = bp.b * a.wg + (int)threadIdx.x;
     if (a.status[chain] != 0) return;
     const ChainParam cp = a.cp[chain];
     double x[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) x[c] = 0.0;
-    if (j < a.N) {
+    if (mine && j < a.N) {
 #pragma unroll
         for (int g = 0; g < ((MODEL >= kSubgroups) ? G : 1); ++g) {
             const Block r = philox((uint32_t)g, (uint32_t)j, kDomainInit, cp.f, cp.k0, cp.k1);
@@ -60,14 +63,16 @@ __global__ __launch_bounds__(WG) void pf_init_kernel(StepArgs a) {
     if (bp.b == 0 && threadIdx.x == 0) a.log_zeta[(size_t)chain * a.T] = 0.0;
     if (a.T > 1) {
         double w = 0.0;
-        if (j < a.N)
+        if (mine && j < a.N)
             w = particle_weight<MODEL, G, OBS>(x, a.Y, cp, a.cp + chain, a.lf, a.lf_max,
                                                a.hidden + (size_t)chain * a.hist_stride + (size_t)j * C);
         const size_t wbase = (size_t)chain * a.wstride;            // buffer 0
         const double loc = block_inclusive_scan<WG>(w, smem);
-        a.wraw[wbase + j] = w;
-        a.wloc[wbase + j] = loc;
-        if (threadIdx.x == WG - 1) a.bsum[(size_t)chain * a.bstride + bp.b] = loc;
+        if (mine) {
+            a.wraw[wbase + j] = w;
+            a.wloc[wbase + j] = loc;
+        }
+        if ((int)threadIdx.x == a.wg - 1) a.bsum[(size_t)chain * a.bstride + bp.b] = loc;
     }
 }
 
@@ -436,8 +441,9 @@ static hipError_t launch_model(const StepArgs& a, int model, int G, int obs, int
     return hipErrorInvalidValue;
 }
 
+// 64-thread init and step blocks; a.wg particles per block: 64, or kGroupBlock for lane-group runs of W >= 8
 hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, const FilterStreams& fs) {
-    if (a.wg != 64) return hipErrorInvalidValue;
+    if (!(a.wg == 64 || (a.wg == kGroupBlock && a.lanes >= 8))) return hipErrorInvalidValue;
     return launch_model<64>(a, model, G, obs, n_chains, fs);
 }
 
