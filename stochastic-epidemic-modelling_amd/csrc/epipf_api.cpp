@@ -247,7 +247,7 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     c->wg = default_wg(n_particles);
     if (const char* e = getenv("EPIPF_SSA_FAST")) c->fast_ssa = atoi(e) != 0;
     if (const char* e = getenv("EPIPF_GROUP_DECIDE")) c->seq_decide = strcmp(e, "seq") == 0;
-    if (const char* e = getenv("EPIPF_CLOCK_SLACK")) c->clock_slack = std::max(1.0f, std::min(1e6f, (float)atof(e)));
+    if (const char* e = getenv("EPIPF_CLOCK_SLACK")) c->clock_slack = std::max(1.0f, std::min(1e12f, (float)atof(e)));
     if (const char* e = getenv("EPIPF_BAND_SLACK")) c->band_slack = std::max(1.0f, std::min(1e4f, (float)atof(e)));
     if (const char* e = getenv("EPIPF_TIE_SCALE")) c->tie_scale = std::max(1.0, std::min(1e300, atof(e)));
     if (const char* e = getenv("EPIPF_STREAMS")) c->n_streams = std::max(1, std::min(kMaxFilterStreams, atoi(e)));

@@ -217,6 +217,45 @@ __device__ __forceinline__ double exact_scale(const F& s, const ChainParam& cp) 
     }
 }
 
+// The certified clock of group_propagate<FASTCLK> (round 4).  The exact loop's tau divides every infection propensity
+// by the population (IEEE) and sum(a) into 1 (IEEE); here the propensities are multiplied by rN = fl(1 / N) instead
+// (a_i' = a_i (1 + e_i), |e_i| <= 3u: fl(q / N) vs fl(q fl(1/N)) for the same q), summed in the same order (positive
+// terms: the partial sums' relative difference grows by <= 2u per term, <= 3u + 2u n_ch), and sum(a')'s reciprocal is
+// still an IEEE division: tau' = tau (1 + e), |e| <= 3u + 2u n_ch + 4u <= 47u for G <= 4 (n_ch <= 20) -- kClockEps =
+// 128u.  The sums t' = fl(t' + tau') then differ from the exact loop's t by at most D_n = (kClockEps + 2.01 u n) t'_n
+// after n events of the step (each add rounds both sides), bounded with margin by (kClockEps + 4u n) 2 tmax near tmax.
+// An event with t' < tmax - D is inside the step as in the exact loop, one with t' > tmax + D outside; in between
+// (probability ~ D times the event rate, ~1e-9 per particle-step) the particle-step is redone on the exact clock.
+constexpr double kClockEps = 0x1.0p-46, kClockPerEvent = 0x1.0p-51;
+
+// sum(a')'s reciprocal (see above); `ok` false when it is not a positive finite number (then the exact clock decides)
+template <int MODEL, int G, class F>
+__device__ __forceinline__ double approx_scale(const F& s, const ChainParam& cp, double rN, bool& ok) {
+    double d;
+    if constexpr (MODEL == kSIR) {
+        d = ((cp.theta[0] * (double)s.S) * (double)s.I) * rN + cp.theta[1] * (double)s.I;
+    } else if constexpr (MODEL == kSEIR) {
+        d = (((cp.theta[0] * (double)s.S) * (double)s.I) * rN + cp.theta[1] * (double)s.E) + cp.theta[2] * (double)s.I;
+    } else {
+        const double gamma = cp.theta[G * G];
+        d = 0.0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+#pragma unroll
+            for (int g2 = 0; g2 < G; ++g2) d = d + ((cp.theta[g * G + g2] * (double)s.S(g2)) * (double)s.I(g)) * rN;
+            d = d + gamma * (double)s.I(g);
+        }
+    }
+    ok = d > 0x1.0p-1000 && d < 0x1.0p1000;
+    return 1.0 / d;
+}
+
+template <int MODEL, int G, class F>
+__device__ __forceinline__ double population_of(const F& s) {
+    if constexpr (MODEL == kSIR || MODEL == kSEIR) return s.N;
+    else return s.sumN;
+}
+
 // One particle over [0, tmax] by its group of W lanes, K events per lane per chunk (call with the whole group
 // active; every lane passes the same parent state x0).  Returns the number of events and the new state in xout, in
 // every lane of the group.  Bit-identical to exact_propagate (and so to the one-lane kernel).
@@ -247,7 +286,9 @@ struct NoDays {
     static constexpr bool kOn = false;
 };
 
-template <int MODEL, int G, int W, int K, class Days = NoDays>
+// FASTCLK (the filter): the certified clock above; returns -1, xout untouched, when a decision is within its bound
+// (the caller then runs the particle-step again with FASTCLK = false, the exact loop's clock).
+template <int MODEL, int G, int W, int K, class Days = NoDays, bool FASTCLK = false>
 __device__ __forceinline__ int group_propagate(const double* x0, double* xout, const ChainParam& cp, uint32_t j,
                                                uint32_t ptag, double tmax, const LogTab* __restrict__ tab,
                                                double* xch, Days* days = nullptr, unsigned long long* ph = nullptr) {
@@ -286,6 +327,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         return 0;
     }
     const float kB = F::kBand * cp.band_slack;           // the decision band (slack 1: kBand, exact in ulo)
+    const double rN = FASTCLK ? 1.0 / population_of<MODEL, G>(st) : 0.0;   // fl(1 / N), once per particle-step
     F mine[K];                                           // mine[k]: state before event k W + gl
 #pragma unroll
     for (int k = 0; k < K; ++k) mine[k] = st;            // the particle-step's constants; the counts kept per event
@@ -354,11 +396,23 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         }
         __builtin_amdgcn_sched_barrier(0);
         EPIPF_PHASE_MARK(tD);
-        double tau[K];                                   // each event's time, the exact loop's expressions
+        double tau[K];                                   // each event's time: the exact loop's expressions, or
+        bool scale_ok = true;                            // FASTCLK's (approx_scale)
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             tau[k] = 0.0;
-            if (k * W + gl < nk) tau[k] = exact_scale<MODEL, G>(mine[k], cp) * L[k];
+            if (k * W + gl < nk) {
+                if constexpr (FASTCLK) {
+                    bool ok;
+                    tau[k] = approx_scale<MODEL, G>(mine[k], cp, rN, ok) * L[k];
+                    scale_ok = scale_ok && ok;
+                } else {
+                    tau[k] = exact_scale<MODEL, G>(mine[k], cp) * L[k];
+                }
+            }
+        }
+        if constexpr (FASTCLK) {                         // group-uniform
+            if ((__ballot(!scale_ok) >> gb) & ((1ull << W) - 1ull)) return -1;
         }
         // t + tau in event order (the exact loop's additions); the step ends at the first t + tau > tmax.  Branch-free:
         // the sum runs on through the chunk (events past nk add tau = 0) and `inside` counts the events before the
@@ -393,19 +447,42 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
                 return true;
             };
             StaticFor<0, E>::run(clock);
-            if (!(tt > tmax)) {
-                inside = E;
+            if constexpr (FASTCLK) {
+                // D: the bound on |t' - t| for the events up to this chunk's end (kClockEps, above; clock_slack >= 1
+                // widens it in tests so that particle-steps take the exact clock on purpose)
+                const double D = (kClockEps + kClockPerEvent * (double)(nev + E)) * (2.0 * tmax) * (double)cp.clock_slack;
+                if (tt < tmax - D) {
+                    inside = E;
+                } else {                                 // the step's last chunk: the first event not surely inside
+                    double t2 = t;
+                    bool alive = true, unsure = false;
+                    auto recount = [&](auto I) __attribute__((always_inline)) -> bool {
+                        constexpr int e = decltype(I)::value;
+                        t2 = t2 + xg[(e / W) * 64 + e % W];
+                        const bool in = t2 < tmax - D;
+                        unsure = unsure || (alive && !in && !(t2 > tmax + D));
+                        alive = alive && in;
+                        inside += alive ? 1 : 0;
+                        return true;
+                    };
+                    StaticFor<0, E>::run(recount);
+                    if (unsure) return -1;               // group-uniform: the same sums in every lane
+                }
             } else {
-                double t2 = t;
-                bool alive = true;
-                auto recount = [&](auto I) __attribute__((always_inline)) -> bool {
-                    constexpr int e = decltype(I)::value;
-                    t2 = t2 + xg[(e / W) * 64 + e % W];
-                    alive = alive && !(t2 > tmax);           // :65-66
-                    inside += alive ? 1 : 0;
-                    return true;
-                };
-                StaticFor<0, E>::run(recount);
+                if (!(tt > tmax)) {
+                    inside = E;
+                } else {
+                    double t2 = t;
+                    bool alive = true;
+                    auto recount = [&](auto I) __attribute__((always_inline)) -> bool {
+                        constexpr int e = decltype(I)::value;
+                        t2 = t2 + xg[(e / W) * 64 + e % W];
+                        alive = alive && !(t2 > tmax);       // :65-66
+                        inside += alive ? 1 : 0;
+                        return true;
+                    };
+                    StaticFor<0, E>::run(recount);
+                }
             }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -548,8 +625,11 @@ __global__ __launch_bounds__(PB * W) void pf_step_group_kernel(StepArgs a, int p
 #pragma unroll
         for (int c = 0; c < C; ++c) x0[c] = (double)rows[pl * C + c];
         const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
-        nev = group_propagate<MODEL, G, W, K>(x0, x, cp, (uint32_t)jg, ptag, 1.0, tab, xch + wave * 64 * K,
-                                              (NoDays*)nullptr, ph);
+        nev = group_propagate<MODEL, G, W, K, NoDays, true>(x0, x, cp, (uint32_t)jg, ptag, 1.0, tab, xch + wave * 64 * K,
+                                                            (NoDays*)nullptr, ph);
+        if (nev < 0)                                     // a clock decision within the certified clock's bound (rare)
+            nev = group_propagate<MODEL, G, W, K, NoDays, false>(x0, x, cp, (uint32_t)jg, ptag, 1.0, tab,
+                                                                 xch + wave * 64 * K, (NoDays*)nullptr, ph);
     }
 #ifdef EPIPF_PHASE_TIMING
     const unsigned long long k2 = __builtin_readcyclecounter();
@@ -609,8 +689,10 @@ static void launch_group_t(const StepArgs& a, int p, dim3 grid, size_t lds, hipS
     hipLaunchKernelGGL((pf_step_group_kernel<MODEL, G, OBS, W, K, 64>), grid, dim3(64 * W), lds, s, a, p);
 }
 
-// (lanes per particle W, events per lane per chunk K) instantiated
-#define EPIPF_GROUP_SHAPES(X) X(2, 1) X(4, 1) X(8, 1) X(16, 1) X(4, 2) X(8, 2) X(16, 2)
+// (lanes per particle W, events per lane per chunk K) instantiated.  K = 2 (round 4, fixed-point pass) measured +4% at
+// config 5 one chain, -1.5% at config 2, -23% at config 5 four chains (profiles/r4c_*): not instantiated, to keep the
+// library's size and build time in check (the code is K-general; add X(w, 2) to bring a shape back).
+#define EPIPF_GROUP_SHAPES(X) X(2, 1) X(4, 1) X(8, 1) X(16, 1)
 
 template <int MODEL, int G, int OBS>
 static GroupStepFn pick_wk(int W, int K) {
