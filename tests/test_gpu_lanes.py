@@ -140,7 +140,9 @@ def test_lane_groups_larger_subgroup_models_equal_one_lane(datasets_golden, G):
         assert int(got[1][0]) == int(ref[1][0])
         np.testing.assert_array_equal(got[2], ref[2])
         np.testing.assert_array_equal(got[3], ref[3])
-        np.testing.assert_array_equal(got[0], ref[0])
+        # equal bit for bit on the same weight layout; with 16-particle blocks (EPIPF_GROUP_BLOCK=16) the step totals
+        # are summed over another tree, an ulp apart -- the oracle comparisons' bar
+        np.testing.assert_allclose(got[0], ref[0], rtol=1e-12, atol=1e-9)
 
 
 @pytest.mark.parametrize("lanes", [2, 16])
