@@ -109,7 +109,6 @@ struct epipf_ctx {
     int lane_events = 0;     // events per lane per chunk of the lane-group kernel: 0 = automatic (EPIPF_LANE_EVENTS)
     int lane_blocks = 1280;  // automatic choice: lane groups up to this many particle blocks per launch
     int group_block = 0;     // lane-group runs' particles per block: 0 = automatic (pick_block), 16 or 64 (EPIPF_GROUP_BLOCK)
-    long group_block_max = 0;  // automatic: 16-particle blocks up to this many per launch (EPIPF_GROUP_BLOCK_MAX)
     int xcd_map = 1;         // XCD-aware placement of the step launches' blocks (EPIPF_XCD_MAP=0: 2-D grid)
     double split_p = -1.0;   // probs of the cached hi/lo split of log p, log1p(-p) (chains usually share probs)
     double split[4] = {0, 0, 0, 0};
@@ -132,14 +131,15 @@ static int pick_lanes(const epipf_ctx* c, int n_chains) {
 }
 
 // Particles per block of a run's weight layout (block sums, in-block prefixes): 64, one wave of the one-lane kernel, or
-// for lane-group runs of W >= 8 that leave CUs idle, kGroupBlock = 16 -- a chain of 10^4 particles is then 626
-// workgroups of 16 W / 64 waves instead of 157 of W waves, spread over all 256 CUs (at most 3 waves per SIMD at W = 16
-// instead of 4 on 157 CUs).  EPIPF_GROUP_BLOCK = 16 / 64 forces it.
-static int pick_block(const epipf_ctx* c, int n_chains, int W) {
+// for W = 16 lane-group runs (at most two chains of 10^4, pick_lanes) kGroupBlock = 16 -- a chain of 10^4 particles is
+// then 626 workgroups of 4 waves instead of 157 of 16 waves, spread over all 256 CUs.  Measured A/B
+// (profiles/r4o_block_clock_ab.txt): W = 16, configs 2 / 3 / 5, one chain +1-2% / +4-6% / +18-20%, two chains 0-2% /
+// 0-5% / +19%; at W = 8 the redundant block-sum scan per workgroup mostly costs more than the spread gains (-2% to -8%).
+// EPIPF_GROUP_BLOCK = 16 / 64 forces either layout for W >= 8.
+static int pick_block(const epipf_ctx* c, int W) {
     if (W < 8) return c->wg;
     if (c->group_block > 0) return c->group_block;
-    const long blocks = (long)n_chains * ((c->N + kGroupBlock - 1) / kGroupBlock);
-    return blocks <= c->group_block_max ? kGroupBlock : c->wg;
+    return W >= 16 ? kGroupBlock : c->wg;
 }
 
 static int pick_lane_events(const epipf_ctx* c, int W) {
@@ -261,7 +261,6 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
         const int b = atoi(e);
         if (b == 0 || b == kGroupBlock || b == 64) c->group_block = b;
     }
-    if (const char* e = getenv("EPIPF_GROUP_BLOCK_MAX")) c->group_block_max = std::max(0L, atol(e));
     if (const char* e = getenv("EPIPF_XCD_MAP")) c->xcd_map = atoi(e) != 0;
     c->B = (n_particles + c->wg - 1) / c->wg;
     if (step_lds_bytes(c->B, c->wg) > 160 * 1024) {
@@ -417,7 +416,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     StepArgs a{};
     a.N = c->N; a.T = c->T; a.max_chains = c->max_chains;
     a.lanes = pick_lanes(c, n_chains);
-    a.wg = pick_block(c, n_chains, a.lanes);
+    a.wg = pick_block(c, a.lanes);
     a.B = (c->N + a.wg - 1) / a.wg;
     a.resample_mode = resample_mode; a.count_events = c->profiling >= EPIPF_PROFILE_COUNTERS ? 1 : 0; a.lf_max = c->lf_max;
     a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride; a.wstride = c->wstride; a.bstride = c->bstride;
