@@ -341,6 +341,7 @@ hipError_t launch_abc_trials(const AbcArgs& a0, hipStream_t s, hipStream_t s2, h
             switch (a.group_lanes) {
                 case 2: hipLaunchKernelGGL(abc_trials_group_kernel<2>, dim3(blocks), dim3(256), 0, s2, a); break;
                 case 8: hipLaunchKernelGGL(abc_trials_group_kernel<8>, dim3(blocks), dim3(256), 0, s2, a); break;
+                case 16: hipLaunchKernelGGL(abc_trials_group_kernel<16>, dim3(blocks), dim3(256), 0, s2, a); break;
                 default: hipLaunchKernelGGL(abc_trials_group_kernel<4>, dim3(blocks), dim3(256), 0, s2, a); break;
             }
             (void)hipEventRecord(join, s2);

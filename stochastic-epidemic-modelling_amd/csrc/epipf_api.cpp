@@ -87,10 +87,9 @@ struct epipf_ctx {
     size_t abc_bytes = 0;
     void* abc = nullptr;
     bool abc_order = true;   // length-ordered ABC lanes (EPIPF_ABC_ORDER=0 disables)
-    // lanes per trial for the longest ABC trials: 0 = automatic (4 for launches of <= kAbcGroupMaxTrials trials,
-    // where the longest trials' lone waves set the launch's length; 1 above), EPIPF_ABC_LANES overrides (1 = off)
+    // lanes per trial for the longest ABC trials: 0 = automatic (abc_launch_trials), EPIPF_ABC_LANES overrides (1 = off)
     int abc_lanes = 0;
-    double abc_group_frac = 0.5, abc_frac = 0.5;   // share of the sorted trials on lane groups (EPIPF_ABC_GROUP_FRAC)
+    double abc_frac = -1.0;  // share of the sorted trials on lane groups: < 0 automatic, EPIPF_ABC_GROUP_FRAC overrides
     bool fast_ssa = true;    // certified f32 event loop (EPIPF_SSA_FAST=0 disables; results are identical)
     bool seq_decide = false; // lane groups: the sequential decision pass instead of the fixed-point one
                              // (EPIPF_GROUP_DECIDE=seq; results are identical, A/B and tests)
@@ -766,15 +765,15 @@ int abc_prepare(epipf_ctx* c, const double* Y, int T, const double* priors, uint
     a.count = c->profiling >= EPIPF_PROFILE_COUNTERS ? 1 : 0;
     c->abc_order = true;
     if (const char* e = getenv("EPIPF_ABC_ORDER")) c->abc_order = atoi(e) != 0;
-    // lane groups for the longest trials (abc_trials_group_kernel): W lanes each for the first `abc_group_frac` of
+    // lane groups for the longest trials (abc_trials_group_kernel): W lanes each for the first `abc_frac` of
     // the sorted trials; EPIPF_ABC_LANES = 1 turns them off (results are identical either way)
     a.group_lanes = c->abc_lanes;                                      // 0: chosen per launch (abc_launch_trials)
     if (const char* e = getenv("EPIPF_ABC_LANES")) {
         const int w = atoi(e);
-        if (w == 1 || w == 2 || w == 4 || w == 8) a.group_lanes = w;
+        if (w == 1 || w == 2 || w == 4 || w == 8 || w == 16) a.group_lanes = w;
     }
-    c->abc_frac = c->abc_group_frac;
-    if (const char* e = getenv("EPIPF_ABC_GROUP_FRAC")) c->abc_frac = std::max(0.0, std::min(1.0, atof(e)));
+    c->abc_frac = -1.0;
+    if (const char* e = getenv("EPIPF_ABC_GROUP_FRAC")) c->abc_frac = atof(e) < 0.0 ? -1.0 : std::min(1.0, atof(e));
     return 0;
 }
 
@@ -814,17 +813,22 @@ int abc_buffers(epipf_ctx* c, int T, int batch, int samples, AbcPlan& p) {
 
 // Launches of up to this many trials put the longest half on lane groups of 4 (automatic mode).  Measured at the
 // reference's setting (profiles/r3_abc_lane_groups.jsonl): 64k-trial launches 5.0 -> 3.1 ms (+61% end to end), 128k
-// +14%, 192k +3.5%, 256k (the default batch) no change -- from there the launch is throughput-bound and the groups'
-// extra instructions per event cancel what they save on the longest trials.
+// +14%, 192k +3.5%.  Larger launches are throughput-bound and take lane groups only for the longest few percent: with
+// round 4's lane-group kernel (fixed-point decisions, early rejection on groups) W = 16 on the longest 4% of a 256k
+// launch runs the reference's setting at 3.06-3.08e7 trials/s against 2.90-2.93e7 one lane (3-8%: 3.0-3.07e7; W = 4
+// or 8, 10% and more lose; profiles/r4q_abc_groups.txt).
 constexpr int kAbcGroupMaxTrials = 196608;
+constexpr int kAbcLongLanes = 16;
+constexpr double kAbcLongFrac = 0.04;
 
 int abc_launch_trials(epipf_ctx* c, AbcArgs& a0, uint32_t t0, int n) {
     AbcArgs& a = a0;
     a.t0 = t0;
     a.n = n;
     const int lanes = a.group_lanes;
-    if (lanes == 0) a.group_lanes = n <= kAbcGroupMaxTrials ? 4 : 1;
-    a.group_end = (a.group_lanes > 1 && a.perm) ? (int)std::llround(c->abc_frac * n) : 0;
+    if (lanes == 0) a.group_lanes = n <= kAbcGroupMaxTrials ? 4 : kAbcLongLanes;
+    const double frac = c->abc_frac >= 0.0 ? c->abc_frac : n <= kAbcGroupMaxTrials ? 0.5 : kAbcLongFrac;
+    a.group_end = (a.group_lanes > 1 && a.perm) ? (int)std::llround(frac * n) : 0;
     if (a.group_end > 0 && !ensure_streams(c, 2)) return fail(EPIPF_EHIP, "auxiliary stream creation failed");
     if (c->profiling) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     hipError_t le = launch_abc_trials(a, c->stream, a.group_end > 0 ? c->aux[1] : nullptr, c->fork, c->join[1]);

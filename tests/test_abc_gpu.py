@@ -143,7 +143,7 @@ def test_abc_large_run_properties(abc_golden, engine):
     np.testing.assert_array_equal(orows[0], traj[-1, :, 1:].astype(np.int32))
 
 
-@pytest.mark.parametrize("lanes,frac", [(2, 0.25), (4, 0.25), (8, 0.25), (4, 1.0), (4, 0.003)])
+@pytest.mark.parametrize("lanes,frac", [(2, 0.25), (4, 0.25), (8, 0.25), (16, 0.25), (4, 1.0), (16, 1.0), (4, 0.003)])
 def test_abc_lane_groups_equal_one_lane_and_oracle(abc_golden, engine, monkeypatch, lanes, frac):
     """The longest trials on lane groups (abc_trials_group_kernel, W lanes per trial, concurrent with the one-lane
     kernel): theta, day tables and distances bit-identical to the one-lane kernel and to the oracle, for every
