@@ -216,6 +216,8 @@ def proposal(meta, kind):
     return meta["h"], meta["sigma"], meta["proposal"]
 
 
+
+
 def timed_chains(ctx, args, cfg, chains, steps, warmup, kind, pipelines=1, streams_env=4):
     """`chains` independent MH chains per rank of BASELINE config `cfg`: warmup, then `steps` timed MH iterations
     between barriers (+ the end-of-run RCCL all-gather of the draws), then one untimed iteration with the device
@@ -343,8 +345,10 @@ def roofline(run, value):
         rocprof_us = pmc.get("trace_avg_us")
         ins = pmc.get("pmc_avg_per_launch", {}).get("SQ_INSTS_VALU")
         units = pmc.get("particle_steps_per_launch")
-        if ins and units:
-            per_ps = ins / units
+        # timed-region profiles (scripts/profile.sh REGION=1) carry the VALU count per counted particle-step itself;
+        # older ones: the launch average over the grid's particle-steps
+        per_ps = pmc.get("valu_per_particle_step") or (ins / units if ins and units else None)
+        if per_ps:
             valu = {"achieved": per_ps * value, "instr_per_particle_step": per_ps,
                     "cycles_per_instr_at_2.4GHz": VALU_PEAK * 2 / (per_ps * value),
                     # VALU pipe busy per SIMD-cycle, SQ_ACTIVE_INST_VALU / GRBM_GUI_ACTIVE of the PMC pass

@@ -39,18 +39,35 @@ def main(d):
                   f"p90 {durs[int(n * .9)]:.1f} p99 {durs[int(n * .99)]:.1f} max {durs[-1]:.1f} "
                   f"sum {sum(durs) / 1e3:.1f} ms; launches > 5x median: {sum(x > 5 * durs[n // 2] for x in durs)}")
     per = defaultdict(lambda: defaultdict(float))   # counter -> dispatch -> value
+    pass_of = {}                                    # counter -> the pass directory it was collected in
     meta = {}
     for p in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
         for r in rows(p):
             if KERNEL not in r["Kernel_Name"]:
                 continue
             per[r["Counter_Name"]][(p, r["Dispatch_Id"])] += float(r["Counter_Value"])
+            pass_of[r["Counter_Name"]] = os.path.relpath(p, d).split(os.sep)[0]
             meta = {k: r.get(k) for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "VGPR_Count",
                                           "SGPR_Count", "Scratch_Size")}
     avg = {k: sum(v.values()) / len(v) for k, v in per.items() if v}
     out["pmc_avg_per_launch"] = avg
     out["pmc_launches"] = {k: len(v) for k, v in per.items()}
     out["dispatch"] = meta
+    # per counted particle-step (profile.sh): the pass's counter total over all its launches / the particle-steps its
+    # bench process ran, count_<pass>.txt -- the bench line's accounting (N x T per chain that runs a filter, degenerate
+    # filters included), whatever the grid of each launch
+    region = {}
+    for k, v in per.items():
+        cp_ = os.path.join(d, f"count_{pass_of.get(k)}.txt")
+        if os.path.exists(cp_):
+            ps = sum(int(line) for line in open(cp_) if line.strip())
+            if ps > 0:
+                region[k] = sum(v.values()) / ps
+    if region:
+        out["per_counted_particle_step"] = True
+        out["pmc_per_particle_step"] = region
+        if "SQ_INSTS_VALU" in region:
+            out["valu_per_particle_step"] = region["SQ_INSTS_VALU"]
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         raw = (avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024.0
         out["hbm_bytes_per_launch"] = raw
@@ -58,7 +75,10 @@ def main(d):
         # per particle-step (LANES lanes per particle): launches of chain groups on concurrent streams have
         # different grid sizes than a one-launch-per-step run, so bench.py scales this figure instead
         lanes = float(meta.get("Grid_Size") or 0) / LANES
-        if lanes > 0:
+        if "FETCH_SIZE" in region and "WRITE_SIZE" in region:
+            out["hbm_bytes_per_particle_step"] = (region["FETCH_SIZE"] + region["WRITE_SIZE"]) * 1024.0
+            out["hbm_bytes_per_particle_step_read_doubled"] = (2 * region["FETCH_SIZE"] + region["WRITE_SIZE"]) * 1024.0
+        elif lanes > 0:
             out["hbm_bytes_per_particle_step"] = raw / lanes
             out["hbm_bytes_per_particle_step_read_doubled"] = out["hbm_bytes_per_launch_read_doubled"] / lanes
     # VALU pipe utilisation (the bound of this kernel): SQ_ACTIVE_INST_VALU counts quad-cycles of VALU

@@ -4,12 +4,28 @@ This is the layer the drop-in `particle_filter` / `particle_mcmc` call.  An engi
 observations, the log-factorial table and the whole particle history resident in HBM; a batched
 `run()` moves only per-chain parameters in and log-likelihoods + status out.
 """
+import atexit
 import ctypes
+import os
 
 import numpy as np
 
 from . import _lib
 from ._lib import check, ptr
+
+# Particle-steps of every epipf_run in this process, counted as bench.py's `value` counts them (N x T per chain that
+# runs a filter; chains passed as inactive count nothing).  With EPIPF_PMC_COUNT=<file> the total is appended to <file>
+# at exit: scripts/profile.sh divides each rocprofv3 pass's counter totals by it (scripts/parse_rocprof.py).
+_PARTICLE_STEPS = [0]
+
+
+def _write_pmc_count():
+    with open(os.environ["EPIPF_PMC_COUNT"], "a") as f:
+        f.write(f"{_PARTICLE_STEPS[0]}\n")
+
+
+if os.environ.get("EPIPF_PMC_COUNT"):
+    atexit.register(_write_pmc_count)
 
 MODEL_IDS = {"sir": _lib.SIR, "seir": _lib.SEIR, "sir_subgroups": _lib.SIR_SUBGROUPS,
              "sir_subgroups2": _lib.SIR_SUBGROUPS2}
@@ -116,6 +132,7 @@ class Engine:
                                 _lib.OBS_NORMAL if observations else _lib.OBS_BINOMIAL, ptr(probs), ptr(keys),
                                 ptr(fidx), ptr(act), mode, ptr(lz), ptr(st)), "epipf_run")
         self._last_n = n
+        _PARTICLE_STEPS[0] += (n if act is None else int(np.count_nonzero(act))) * self.N * self.T
         return lz, st
 
     def history(self, n_chains=None):
