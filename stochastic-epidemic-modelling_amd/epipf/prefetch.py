@@ -117,11 +117,13 @@ def _value(src):
     return np.exp(lz[-1]), lz[-1], src.result[2]
 
 
-def expected_iterations(slots, alphas):
+def expected_iterations(slots, alphas, deltas=None):
     """Expected MH iterations one round commits when `slots` filters are scheduled best-first over chains whose
-    accept probability is `alphas` (the scheduler of PrefetchSampler._schedule on the ideal tree: every node a
-    filter, path probability = product of a / 1 - a along it; a round commits the realised path's evaluated
-    prefix, so the expectation is the sum of the scheduled nodes' path probabilities)."""
+    accept probability is `alphas` and whose filters degenerate with probability `deltas` (the scheduler of
+    PrefetchSampler._schedule on the ideal tree: every node a filter with three outcomes -- degenerate (d), accepted
+    ((1 - d) a), rejected ((1 - d)(1 - a)) -- path probability = product along it; a round commits the realised path's
+    evaluated prefix, so the expectation is the sum of the scheduled nodes' path probabilities)."""
+    deltas = [0.0] * len(alphas) if deltas is None else deltas
     heap = [(-1.0, c) for c in range(len(alphas))]
     heapq.heapify(heap)
     e = 0.0
@@ -130,9 +132,11 @@ def expected_iterations(slots, alphas):
             break
         negp, c = heapq.heappop(heap)
         e -= negp
-        a = alphas[c]
-        heapq.heappush(heap, (negp * a, c))
-        heapq.heappush(heap, (negp * (1.0 - a), c))
+        a, d = alphas[c], deltas[c]
+        heapq.heappush(heap, (negp * (1.0 - d) * a, c))
+        heapq.heappush(heap, (negp * (1.0 - d) * (1.0 - a), c))
+        if d > 0.0:
+            heapq.heappush(heap, (negp * d, c))
     return e
 
 
@@ -142,10 +146,12 @@ class SlotTuner:
     the chip's fill set where), and its yield E(K) (expected_iterations) grows sub-linearly at a rate set by the
     acceptance rate, so the best K depends on both; T(K) is measured on the chain's own rounds -- each candidate power
     of two run once to warm up (not timed: a first launch shape pays one-off costs) and then `tries` times, T(K) the
-    fastest of its last three rounds; the best and its neighbours re-measured every `refresh` rounds -- and E(K) comes
-    from the chains' running acceptance rates."""
+    median of its last five rounds (a round lasts as long as its slowest filter, and the filters' costs vary with their
+    theta: at config 5's h = 1 a fastest-of-three estimate picked 4 slots in one run and 1 in another, 0.78e8 against
+    1.10e8 particle-steps/s, profiles/r4y_prefetch_cfg5.txt); the best and its neighbours re-measured every `refresh`
+    rounds -- and E(K) comes from the chains' running acceptance rates."""
 
-    def __init__(self, lo, hi, tries=2, refresh=24):
+    def __init__(self, lo, hi, tries=3, refresh=24):
         self.cands = sorted({lo} | {k for k in (1, 2, 4, 8, 16, 32, 64, 128) if lo <= k <= hi} | {hi})
         self.samples = {k: [] for k in self.cands}          # K -> the last round times (s)
         self.count = {k: 0 for k in self.cands}              # rounds run at K (the first is a warm-up)
@@ -154,13 +160,13 @@ class SlotTuner:
         self.best = None
 
     def time(self, k):
-        return min(self.samples[k][-3:])
+        return float(np.median(self.samples[k][-5:]))
 
-    def pick(self, alphas):
+    def pick(self, alphas, deltas=None):
         for k in self.cands:                                # exploration: every candidate measured `tries` times
             if len(self.samples[k]) < self.tries:
                 return k
-        rate = {k: expected_iterations(k, alphas) / self.time(k) for k in self.cands}
+        rate = {k: expected_iterations(k, alphas, deltas) / self.time(k) for k in self.cands}
         self.best = max(self.cands, key=lambda k: rate[k])
         if self.rounds % self.refresh == 0:                 # keep the neighbours' times current
             i = self.cands.index(self.best)
@@ -175,7 +181,7 @@ class SlotTuner:
             return
         self.count[k] += 1
         if self.count[k] > 1:
-            self.samples[k] = (self.samples[k] + [seconds])[-3:]
+            self.samples[k] = (self.samples[k] + [seconds])[-5:]
 
 
 class PrefetchSampler(ChainSampler):
@@ -202,6 +208,7 @@ class PrefetchSampler(ChainSampler):
         self.rounds = 0
         self.speculative_filters = 0
         self.degenerate = 0                                     # realised filters that returned (None, None, None)
+        self.degenerate_c = [0] * self.nc                       # the same per chain (the scheduler's third branch)
 
     # ------------------------------------------------------------------ host draws
     def _factor(self, std):
@@ -264,7 +271,24 @@ class PrefetchSampler(ChainSampler):
 
     # ------------------------------------------------------------------ rounds
     def _alpha(self, c):
-        return (self.acceptances[c] - 1 + 1.0) / (self.filters_run[c] + 2.0)
+        """Accept probability of a chain's filter that did not degenerate."""
+        ok = self.filters_run[c] - self.degenerate_c[c]
+        return (self.acceptances[c] - 1 + 1.0) / (ok + 2.0)
+
+    def _delta(self, c):
+        """Probability that a chain's filter degenerates (all weights 0: pmcmc.py:187-192), the realised rate.  At
+        config 5's h = 1 about a fifth of the filters do (profiles/r4v_chain_cost_cfg5.txt), and their subtree forks
+        the RNG stream (no path pick, no acceptance uniform), so a tree of accept / reject branches alone commits
+        about 1 / 0.2 iterations per round whatever its width."""
+        return self.degenerate_c[c] / (self.filters_run[c] + 2.0)
+
+    def _push_children(self, heap, x, p):
+        """The unevaluated filter node x's three outcomes, best-first by path probability."""
+        a, d = self._alpha(x.chain), self._delta(x.chain)
+        heapq.heappush(heap, (-p * (1.0 - d) * a, next(self._tick), x.kids[0]))
+        heapq.heappush(heap, (-p * (1.0 - d) * (1.0 - a), next(self._tick), x.kids[1]))
+        if d > 0.0:
+            heapq.heappush(heap, (-p * d, next(self._tick), self._degenerate_child(x)))
 
     def _schedule(self):
         heap = []
@@ -282,14 +306,12 @@ class PrefetchSampler(ChainSampler):
                 continue
             if x.result is None:
                 out.append(x)
-                a = self._alpha(x.chain)
-                heapq.heappush(heap, (-p * a, next(self._tick), x.kids[0]))
-                heapq.heappush(heap, (-p * (1.0 - a), next(self._tick), x.kids[1]))
+                self._push_children(heap, x, p)
                 continue
             y = self._decision(x)
             if y is not None:
                 heapq.heappush(heap, (-p, next(self._tick), y))
-            else:
+            else:                                               # its filter ran and did not degenerate
                 a = self._alpha(x.chain)
                 heapq.heappush(heap, (-p * a, next(self._tick), x.kids[0]))
                 heapq.heappush(heap, (-p * (1.0 - a), next(self._tick), x.kids[1]))
@@ -349,6 +371,7 @@ class PrefetchSampler(ChainSampler):
                     y = self._decision(x)
                     ok = x.result[1] == _lib.STATUS_OK
                     self.degenerate += 0 if ok else 1
+                    self.degenerate_c[c] += 0 if ok else 1
                     self._commit(c, x, y, True, ok and y is x.kids[0])
                 x = y
                 done += 1
@@ -371,7 +394,8 @@ class PrefetchSampler(ChainSampler):
         if self.tuner is not None:
             import time
             t0 = time.perf_counter()
-            self.slots = self.tuner.pick([self._alpha(c) for c in range(self.nc)])
+            self.slots = self.tuner.pick([self._alpha(c) for c in range(self.nc)],
+                                         [self._delta(c) for c in range(self.nc)])
         nodes = self._schedule()
         if nodes:
             self._evaluate(nodes)

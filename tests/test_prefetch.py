@@ -152,10 +152,13 @@ def test_expected_iterations_model():
     assert pf.expected_iterations(2, [0.6]) == pytest.approx(1.6)
     assert pf.expected_iterations(5, [0.0]) == pytest.approx(5.0)
     assert pf.expected_iterations(3, [0.5, 0.5]) == pytest.approx(2.5)
+    # a third branch for degenerate filters (probability d): the root, then its degenerate child (0.5), then 0.25
+    assert pf.expected_iterations(3, [0.5], [0.5]) == pytest.approx(1.75)
+    assert pf.expected_iterations(4, [0.3], [0.0]) == pytest.approx(pf.expected_iterations(4, [0.3]))
 
 
 def test_slot_tuner_picks_the_best_measured_rate():
-    """After exploring every candidate twice, the tuner takes the width with the most expected iterations per second:
+    """After exploring every candidate three times, the tuner takes the width with the most expected iterations per second:
     with round times flat up to 4 slots and linear beyond, 4 wins at acceptance 0.5."""
     t = pf.SlotTuner(1, 16)
     cost = {1: 1.0, 2: 1.0, 4: 1.0, 8: 2.0, 16: 4.0}
