@@ -121,12 +121,15 @@ struct epipf_ctx {
 // +3% / 0% / +9%; at 8 chains W = 4 leads by 16-29%: profiles/r3k_lanes_sweep_chains.jsonl).  Since round 4's
 // fixed-point decision pass (a chunk's decisions cost ~2.3 evaluations instead of W dependent ones) and the clock pass
 // through LDS, W = 16 leads up to two chains of 10^4 (320 blocks; one chain: configs 2 / 3 / 5 +12% / +16% / +18%
-// over W = 8, two chains +9% / +10% / +12%), W = 8 from three (profiles/r4i_*, r4k_*).
+// over W = 8, two chains +9% / +10% / +12%), W = 8 from three (profiles/r4i_*, r4k_*).  With W = 16 on 16-particle
+// blocks (pick_block) the subgroup models keep W = 16 up to four chains (+27% over W = 8 at three and four) and SIR /
+// SEIR take W = 8 up to six (+11% / +7% over W = 4 at six; profiles/r4aa_lanes_sweep.txt).
 static int pick_lanes(const epipf_ctx* c, int n_chains) {
     if (c->lanes > 0) return c->lanes;
-    const long blocks = (long)n_chains * c->B;
-    return blocks <= (long)c->lane_blocks / 4 ? 16 : blocks <= (long)c->lane_blocks / 2 ? 8
-         : blocks <= (long)c->lane_blocks ? 4 : 1;
+    const long blocks = (long)n_chains * c->B, lb = c->lane_blocks;
+    if (c->model == EPIPF_SIR || c->model == EPIPF_SEIR)
+        return blocks <= lb / 4 ? 16 : blocks <= lb * 3 / 4 ? 8 : blocks <= lb ? 4 : 1;
+    return blocks <= lb / 2 ? 16 : blocks <= lb ? 4 : 1;
 }
 
 // Particles per block of a run's weight layout (block sums, in-block prefixes): 64, one wave of the one-lane kernel, or

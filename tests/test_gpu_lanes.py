@@ -207,7 +207,11 @@ def test_lane_groups_full_size_single_chain_vs_oracle(cfg, lanes):
     obs = bool(meta.get("observations", False))
     lz, st = eng.run(theta_vector(mid, ref_th)[0][None], [meta["probs"]], [4242], [7], observations=obs)
     blocks = (meta["N"] + 63) // 64
-    assert eng.stats()["last_lanes"] == (lanes or (16 if blocks <= 320 else 8 if blocks <= 640 else 4))
+    if mid < 2:                                          # SIR / SEIR
+        auto = 16 if blocks <= 320 else 8 if blocks <= 960 else 4
+    else:
+        auto = 16 if blocks <= 640 else 4
+    assert eng.stats()["last_lanes"] == (lanes or auto)
     hid, anc = eng.history(1)
     eng.close()
     o = oracle.particle_filter(Y, meta["model"], ref_th, obs, meta["probs"], meta["N"], meta["n_population"],
@@ -219,15 +223,23 @@ def test_lane_groups_full_size_single_chain_vs_oracle(cfg, lanes):
 
 
 def test_automatic_lane_choice():
-    """Up to two chains of 10^4 particles get 16 lanes, up to 4 chains 8, up to 8 chains 4; a batch that fills the chip
-    keeps one lane per particle."""
+    """SIR / SEIR: up to two chains of 10^4 particles get 16 lanes, up to 6 chains 8, up to 8 chains 4; subgroup models:
+    16 lanes up to 4 chains, then 4 up to 8; a batch that fills the chip keeps one lane per particle."""
     from epipf.engine import Engine
     Y = np.zeros((3, 3))
     eng = Engine("sir", 1, 10000, 3, 256)
     eng.set_observations(Y)
     eng.set_population(10000, 20)
-    for chains, want in [(1, 16), (2, 16), (3, 8), (4, 8), (5, 4), (8, 4), (9, 1), (256, 1)]:
+    for chains, want in [(1, 16), (2, 16), (3, 8), (4, 8), (6, 8), (7, 4), (8, 4), (9, 1), (256, 1)]:
         eng.run(np.tile([0.25, 0.1], (chains, 1)), [0.1] * chains, list(range(1, chains + 1)), [0] * chains)
+        assert eng.stats()["last_lanes"] == want, (chains, eng.stats()["last_lanes"])
+    eng.close()
+    eng = Engine("sir_subgroups", 2, 10000, 3, 16)
+    eng.set_observations(np.zeros((3, 6)))
+    eng.set_population([2000, 3000], [20, 30])
+    th = np.array([4.0, 1.0, 1.0, 4.0, 1.0])
+    for chains, want in [(1, 16), (4, 16), (5, 4), (8, 4), (9, 1)]:
+        eng.run(np.tile(th, (chains, 1)), [0.1] * chains, list(range(1, chains + 1)), [0] * chains)
         assert eng.stats()["last_lanes"] == want, (chains, eng.stats()["last_lanes"])
     eng.close()
 
