@@ -86,6 +86,14 @@ class _Stream:
         return f
 
 
+class _DegRef:
+    """A degenerate-filter child in the scheduler's heap, created (a stream fork: RandomState replay) only once popped."""
+    __slots__ = ("x",)
+
+    def __init__(self, x):
+        self.x = x
+
+
 class _Node:
     """State before MH iteration `i` on one path of one chain's outcome tree."""
     __slots__ = ("chain", "i", "parent", "theta", "src", "stream", "k", "fnext", "chosen", "u", "prop", "neg",
@@ -288,7 +296,7 @@ class PrefetchSampler(ChainSampler):
         heapq.heappush(heap, (-p * (1.0 - d) * a, next(self._tick), x.kids[0]))
         heapq.heappush(heap, (-p * (1.0 - d) * (1.0 - a), next(self._tick), x.kids[1]))
         if d > 0.0:
-            heapq.heappush(heap, (-p * d, next(self._tick), self._degenerate_child(x)))
+            heapq.heappush(heap, (-p * d, next(self._tick), _DegRef(x)))
 
     def _schedule(self):
         heap = []
@@ -298,6 +306,8 @@ class PrefetchSampler(ChainSampler):
         while heap and len(out) < self.slots:
             negp, _, x = heapq.heappop(heap)
             p = -negp
+            if isinstance(x, _DegRef):
+                x = self._degenerate_child(x.x)
             if x.i >= self.iters:
                 continue
             self._expand(x)
