@@ -61,7 +61,9 @@ def parse():
                          "others' filters (epipf.pmcmc.run_pipelined); 1 = one lockstep sampler; 0 = automatic: 2 "
                          "where the MH step is host-bound (config 1: tiny filters), else 1 (DESIGN.md §6)")
     ap.add_argument("--prefetch", type=int, default=16, help="filter slots per round of the speculative single chain")
-    ap.add_argument("--prefetch-iters", type=int, default=60, help="MH iterations timed for the speculative chain")
+    # ~20 rounds: a speculative round commits ~10 iterations at config 2, so 60 iterations were 6 rounds and the
+    # adaptive width's figure moved by +-20% from run to run (profiles/r4y_prefetch_cfg5.txt)
+    ap.add_argument("--prefetch-iters", type=int, default=200, help="MH iterations timed for the speculative chain")
     return ap.parse_args()
 
 
@@ -443,7 +445,7 @@ def config_runs(ctx, args):
                 entry["fixed_theta"] = run_summary(run)
         if chains == 1 and ctx.rank == 0 and ctx.world == 1:
             entry["prefetch_auto"] = prefetch_chain(args, run["Y"], run["meta"], run["N"], run["T"], ctx.local, "auto",
-                                                    40, h=entry["h"], sigma=run["meta"]["sigma"])
+                                                    160, h=entry["h"], sigma=run["meta"]["sigma"])
         out[name] = entry
     return out
 
