@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: the next chunk's draws issued during the clock pass (group_propagate).  Parity first (lane-group tests, ABC
+# Round 4 A/B of this tree against ab_old/ (the previous commit's build).  Parity first (lane-group tests, ABC
 # lane tests, the random fuzz sweep), then lanes sweeps of ab_old/ (previous commit) vs this tree, alternating.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -7,7 +7,7 @@ OUT=gpurun_out/${TAG:-r4ae}; mkdir -p $OUT
 export TMPDIR=/tmp
 ROOT=$(pwd)
 if [ -z "${SKIP_TESTS:-}" ]; then
-  timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_lanes.py tests/test_gpu_fuzz.py tests/test_abc_gpu.py > $OUT/pytest.log 2>&1 || { echo "TESTS FAILED"; tail -40 $OUT/pytest.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread ${TESTS:-tests/test_gpu_lanes.py tests/test_gpu_fuzz.py tests/test_abc_gpu.py} > $OUT/pytest.log 2>&1 || { echo "TESTS FAILED"; tail -40 $OUT/pytest.log; exit 1; }
   tail -1 $OUT/pytest.log
 fi
 for i in ${ROUNDS:-1 2}; do

@@ -153,8 +153,8 @@ static int pick_lane_events(const epipf_ctx* c, int W) {
 // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp): D bounds the depth of the parallel
 // reduction tree behind every prefix: in-block scan (6 shuffle levels + <=4 wave offsets + 1) = 11 <= 16,
 // block-sum scan 16 + 2 * ceil(B / WG) sequential chunk adds, +2 for the final adds.
-static double cert_k(int N, int B, int wg) {
-    const int S = prefix_segment(B), nseg = (B + S - 1) / S;
+static double cert_k(int N, int B, int S, int wg) {
+    const int nseg = (B + S - 1) / S;
     const int per = ((nseg + wg - 1) / wg) * S;          // sequential block-sum adds per lane (scan_segments)
     const int D = 34 + 2 * per;
     return (double)N + 2.0 * D + 8.0;
@@ -422,13 +422,16 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     a.B = (c->N + a.wg - 1) / a.wg;
     a.resample_mode = resample_mode; a.count_events = c->profiling >= EPIPF_PROFILE_COUNTERS ? 1 : 0; a.lf_max = c->lf_max;
     a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride; a.wstride = c->wstride; a.bstride = c->bstride;
-    a.cert_k = cert_k(c->N, a.B, 64);                     // the block-sum scans run on 64 lanes whatever the layout
+    // S blocks per prefix segment: 1 (every block sum in LDS) for lane-group runs on 16-particle blocks up to
+    // kMaxFlatGroupBlocks, else the smallest power of two with at most kMaxSegments segments
+    a.seg = (a.lanes > 1 && a.wg == kGroupBlock && a.B <= kMaxFlatGroupBlocks) ? 1 : prefix_segment(a.B);
+    a.nseg = (a.B + a.seg - 1) / a.seg;
+    a.cert_k = cert_k(c->N, a.B, a.seg, 64);              // the block-sum scans run on 64 lanes whatever the layout
     // the reference-ambiguity test runs with the other device counters (bench.py's untimed counters iteration, the
     // parity tests); ref_k = 0 switches it off in the timed, production launches
     a.ref_k = a.count_events ? 2.0 * ref_pmf_envelope(obs_model, c->lf_max) * (1.0 + 0x1.0p-10) : 0.0;
     a.Y = c->Y; a.lf = c->lf; a.logtab = c->logtab; a.cp = c->cp; a.hidden = c->hidden; a.ancestry = c->ancestry;
     a.wraw = c->wraw; a.wloc = c->wloc; a.bsum = c->bsum; a.log_zeta = c->log_zeta; a.status = c->status;
-    a.seg = prefix_segment(a.B); a.nseg = (a.B + a.seg - 1) / a.seg;
     a.counters = c->counters;
     a.lane_events = pick_lane_events(c, a.lanes);
     a.xcd_map = c->xcd_map;
@@ -699,7 +702,7 @@ int epipf_resample(epipf_ctx* c, int n, const double* w, const double* u, int32_
     if (ensure_scratch(c, need)) return EPIPF_ENOMEM;
     char* p = (char*)c->scratch;
     ResampleArgs a{};
-    a.N = n; a.B = B; a.cert_k = cert_k(n, B, 256);
+    a.N = n; a.B = B; a.cert_k = cert_k(n, B, prefix_segment(B), 256);
     double* dw = (double*)p; p += nw;
     double* du = (double*)p; p += nw;
     a.wraw = (double*)p; p += nw;

@@ -520,8 +520,8 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
 
 // LDS of the lane-group step kernel: log table | tau exchange [W][K][64] | red[16] | particle rows [64][C] int32 |
 // block-sum prefix
-inline size_t group_lds_bytes_impl(int B, int C, int W, int K) {
-    return step_lds_bytes(B, 64) + sizeof(int32_t) * 64 * (size_t)C + sizeof(double) * 64 * (size_t)W * K;
+inline size_t group_lds_bytes_impl(int B, int S, int C, int W, int K) {
+    return step_lds_bytes_seg(B, S, 64) + sizeof(int32_t) * 64 * (size_t)C + sizeof(double) * 64 * (size_t)W * K;
 }
 
 // PB particles per block: 64 (the one-lane kernel's blocks), or kGroupBlock = 16 for runs that would leave CUs idle

@@ -177,13 +177,18 @@ void logfact_table(int n_max, double* out);
 void log_p_split(double p, double* logp_hi, double* logp_lo, double* log1mp_hi, double* log1mp_lo);
 
 size_t step_lds_bytes(int B, int wg);
+size_t step_lds_bytes_seg(int B, int S, int wg);   // with S blocks per prefix segment (1: block sums in LDS)
 // lane-group step kernel (epipf_group.hip): W lanes per particle, launched as grid (B, chains) x 64 W threads
 using GroupStepFn = void (*)(const StepArgs& a, int p, dim3 grid, size_t lds, hipStream_t s);
 GroupStepFn group_step_launcher(int model, int G, int obs, int W, int K);
 bool group_shape_supported(int W, int K);
-size_t group_lds_bytes(int B, int C, int W, int K);
+size_t group_lds_bytes(int B, int S, int C, int W, int K);
 int prefix_segment(int B);
 constexpr int kMaxSegments = 200;
+// lane-group runs on 16-particle blocks keep every block sum and its prefix in LDS (S = 1) up to this many blocks
+// (2 x 8 B each): a chain of 10^4 particles is 626 blocks, whose segmented prefix (S = 4) cost each workgroup's
+// resampling search a dependent global load of its segment's block sums
+constexpr int kMaxFlatGroupBlocks = 1280;
 constexpr int kGroupBlock = 16;   // particles per block of the lane-group runs that spread a chain over every CU
 hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, const FilterStreams& fs);
 hipError_t launch_path_sample(const PathArgs& a, hipStream_t s);

@@ -359,8 +359,9 @@ int prefix_segment(int B) {
     return S;
 }
 
-size_t step_lds_bytes(int B, int wg) {
-    const int S = prefix_segment(B);
+size_t step_lds_bytes(int B, int wg) { return step_lds_bytes_seg(B, prefix_segment(B), wg); }
+
+size_t step_lds_bytes_seg(int B, int S, int wg) {
     if (S == 1) return sizeof(LogTab) * kLogTabEntries + sizeof(double) * (size_t)(16 + B + B + wg);
     return sizeof(LogTab) * kLogTabEntries + sizeof(double) * (size_t)(16 + 2 * ((B + S - 1) / S));
 }
@@ -379,7 +380,7 @@ static hipError_t launch_filter_t(const StepArgs& a, int n_chains, const FilterS
     // W lanes per particle (runs too small to fill the chip): the lane-group step kernel, epipf_group.hip
     const GroupStepFn group = a.lanes > 1 ? group_step_launcher(MODEL, G, OBS, a.lanes, a.lane_events) : nullptr;
     if (a.lanes > 1 && !group) return hipErrorInvalidValue;
-    const size_t glds = group ? group_lds_bytes(a.B, C, a.lanes, a.lane_events) : 0;
+    const size_t glds = group ? group_lds_bytes(a.B, a.seg, C, a.lanes, a.lane_events) : 0;
     for (int g = 0; g < S; ++g) {
         StepArgs ag = a;
         ag.chain0 = (int)((long)n_chains * g / S);
