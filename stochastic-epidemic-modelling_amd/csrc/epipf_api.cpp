@@ -140,7 +140,6 @@ static int pick_lanes(const epipf_ctx* c, int n_chains) {
 // EPIPF_GROUP_BLOCK = 16 / 64 forces either layout for W >= 8.
 static int pick_block(const epipf_ctx* c, int W) {
     if (W < 8) return c->wg;
-    if (c->group_block == kGroupBlockSmall) return W >= 16 ? kGroupBlockSmall : kGroupBlock;
     if (c->group_block > 0) return c->group_block;
     return W >= 16 ? kGroupBlock : c->wg;
 }
@@ -262,7 +261,7 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     if (const char* e = getenv("EPIPF_LANE_EVENTS")) c->lane_events = std::max(0, atoi(e));
     if (const char* e = getenv("EPIPF_GROUP_BLOCK")) {
         const int b = atoi(e);
-        if (b == 0 || b == kGroupBlockSmall || b == kGroupBlock || b == 64) c->group_block = b;
+        if (b == 0 || b == kGroupBlock || b == 64) c->group_block = b;
     }
     if (const char* e = getenv("EPIPF_XCD_MAP")) c->xcd_map = atoi(e) != 0;
     c->B = (n_particles + c->wg - 1) / c->wg;
@@ -274,7 +273,7 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     c->anc_stride = (size_t)t_max * n_particles;
     c->wstride = (size_t)c->B * c->wg;
     // block sums for the lane-group runs' 16-particle blocks too (pick_block, kGroupBlock)
-    c->bstride = std::max((size_t)c->B, (size_t)((n_particles + kGroupBlockSmall - 1) / kGroupBlockSmall));
+    c->bstride = std::max((size_t)c->B, (size_t)((n_particles + kGroupBlock - 1) / kGroupBlock));
     int rc = 0;
     if (hipSetDevice(device) != hipSuccess) { free_ctx(c); return fail(EPIPF_EHIP, "hipSetDevice(%d) failed", device); }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -425,7 +424,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride; a.wstride = c->wstride; a.bstride = c->bstride;
     // S blocks per prefix segment: 1 (every block sum in LDS) for lane-group runs on 16-particle blocks up to
     // kMaxFlatGroupBlocks, else the smallest power of two with at most kMaxSegments segments
-    a.seg = (a.lanes > 1 && a.wg < 64 && a.B <= kMaxFlatGroupBlocks) ? 1 : prefix_segment(a.B);
+    a.seg = (a.lanes > 1 && a.wg == kGroupBlock && a.B <= kMaxFlatGroupBlocks) ? 1 : prefix_segment(a.B);
     a.nseg = (a.B + a.seg - 1) / a.seg;
     a.cert_k = cert_k(c->N, a.B, a.seg, 64);              // the block-sum scans run on 64 lanes whatever the layout
     // the reference-ambiguity test runs with the other device counters (bench.py's untimed counters iteration, the

@@ -1391,13 +1391,13 @@ __device__ __forceinline__ double ref_halfwidth(double v, double ref_k) {
 // those <= Ut); counting a monotone predicate is the binary search's answer.
 template <int WG, bool FLAT = false>
 __device__ __forceinline__ int inblock_search(double base, const double* __restrict__ L, double Ut) {
-    if constexpr (FLAT && WG <= 16) {                   // 8- / 16-particle blocks: one round of WG - 1 independent loads
-        double c[WG - 1];
+    if constexpr (FLAT && WG == 16) {                   // 16-particle blocks: one round of 15 independent loads
+        double c[15];
 #pragma unroll
-        for (int i = 0; i < WG - 1; ++i) c[i] = L[i];
+        for (int i = 0; i < 15; ++i) c[i] = L[i];
         int o = 0;
 #pragma unroll
-        for (int i = 0; i < WG - 1; ++i) o += (base + c[i] > Ut) ? 0 : 1;
+        for (int i = 0; i < 15; ++i) o += (base + c[i] > Ut) ? 0 : 1;
         return o;
     } else if constexpr (FLAT) {
         static_assert(WG == 64, "8 x 8 sub-blocks");

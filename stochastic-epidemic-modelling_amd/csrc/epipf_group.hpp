@@ -682,13 +682,6 @@ __global__ __launch_bounds__(PB * W) void pf_step_group_kernel(StepArgs a, int p
 // ------------------------------------------------------------------------------- launch table
 template <int MODEL, int G, int OBS, int W, int K>
 static void launch_group_t(const StepArgs& a, int p, dim3 grid, size_t lds, hipStream_t s) {
-    if constexpr (W >= 16) {                             // 8-particle blocks (a.wg, pick_block): W = 16 only
-        if (a.wg == kGroupBlockSmall) {
-            hipLaunchKernelGGL((pf_step_group_kernel<MODEL, G, OBS, W, K, kGroupBlockSmall>), grid,
-                               dim3(kGroupBlockSmall * W), lds, s, a, p);
-            return;
-        }
-    }
     if constexpr (W >= 8) {                              // 16-particle blocks (a.wg, pick_block): W >= 8 only
         if (a.wg == kGroupBlock) {
             hipLaunchKernelGGL((pf_step_group_kernel<MODEL, G, OBS, W, K, kGroupBlock>), grid, dim3(kGroupBlock * W), lds,

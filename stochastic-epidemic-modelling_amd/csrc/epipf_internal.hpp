@@ -190,7 +190,6 @@ constexpr int kMaxSegments = 200;
 // resampling search a dependent global load of its segment's block sums
 constexpr int kMaxFlatGroupBlocks = 1280;
 constexpr int kGroupBlock = 16;   // particles per block of the lane-group runs that spread a chain over every CU
-constexpr int kGroupBlockSmall = 8;   // the same for W = 16 (two-wave workgroups; EPIPF_GROUP_BLOCK=8)
 hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, const FilterStreams& fs);
 hipError_t launch_path_sample(const PathArgs& a, hipStream_t s);
 hipError_t launch_simulate(const SimArgs& a, int model, int G, hipStream_t s);

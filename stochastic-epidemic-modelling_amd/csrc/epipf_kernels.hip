@@ -442,11 +442,9 @@ static hipError_t launch_model(const StepArgs& a, int model, int G, int obs, int
     return hipErrorInvalidValue;
 }
 
-// 64-thread init and step blocks; a.wg particles per block: 64, kGroupBlock for lane-group runs of W >= 8, or
-// kGroupBlockSmall for W = 16
+// 64-thread init and step blocks; a.wg particles per block: 64, or kGroupBlock for lane-group runs of W >= 8
 hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, const FilterStreams& fs) {
-    if (!(a.wg == 64 || (a.wg == kGroupBlock && a.lanes >= 8) || (a.wg == kGroupBlockSmall && a.lanes >= 16)))
-        return hipErrorInvalidValue;
+    if (!(a.wg == 64 || (a.wg == kGroupBlock && a.lanes >= 8))) return hipErrorInvalidValue;
     return launch_model<64>(a, model, G, obs, n_chains, fs);
 }
 
