@@ -125,6 +125,26 @@ def _value(src):
     return np.exp(lz[-1]), lz[-1], src.result[2]
 
 
+def expected_iterations_upto(kmax, alphas, deltas=None):
+    """[E(1), ..., E(kmax)] of expected_iterations from one best-first expansion (the scheduled nodes of K slots are
+    the first K of K + 1's)."""
+    deltas = [0.0] * len(alphas) if deltas is None else deltas
+    heap = [(-1.0, c) for c in range(len(alphas))]
+    heapq.heapify(heap)
+    e, out = 0.0, []
+    for _ in range(int(kmax)):
+        if heap:
+            negp, c = heapq.heappop(heap)
+            e -= negp
+            a, d = alphas[c], deltas[c]
+            heapq.heappush(heap, (negp * (1.0 - d) * a, c))
+            heapq.heappush(heap, (negp * (1.0 - d) * (1.0 - a), c))
+            if d > 0.0:
+                heapq.heappush(heap, (negp * d, c))
+        out.append(e)
+    return out
+
+
 def expected_iterations(slots, alphas, deltas=None):
     """Expected MH iterations one round commits when `slots` filters are scheduled best-first over chains whose
     accept probability is `alphas` and whose filters degenerate with probability `deltas` (the scheduler of
@@ -159,13 +179,14 @@ class SlotTuner:
     1.10e8 particle-steps/s, profiles/r4y_prefetch_cfg5.txt); the best and its neighbours re-measured every `refresh`
     rounds -- and E(K) comes from the chains' running acceptance rates."""
 
-    def __init__(self, lo, hi, tries=3, refresh=24):
+    def __init__(self, lo, hi, tries=3, refresh=24, reeval=8):
         self.cands = sorted({lo} | {k for k in (1, 2, 4, 8, 16, 32, 64, 128) if lo <= k <= hi} | {hi})
         self.samples = {k: [] for k in self.cands}          # K -> the last round times (s)
         self.count = {k: 0 for k in self.cands}              # rounds run at K (the first is a warm-up)
-        self.tries, self.refresh = tries, refresh
+        self.tries, self.refresh, self.reeval = tries, refresh, reeval
         self.rounds = 0
         self.best = None
+        self._next_eval = 0
 
     def time(self, k):
         return float(np.median(self.samples[k][-5:]))
@@ -174,13 +195,19 @@ class SlotTuner:
         for k in self.cands:                                # exploration: every candidate measured `tries` times
             if len(self.samples[k]) < self.tries:
                 return k
-        rate = {k: expected_iterations(k, alphas, deltas) / self.time(k) for k in self.cands}
-        self.best = max(self.cands, key=lambda k: rate[k])
-        if self.rounds % self.refresh == 0:                 # keep the neighbours' times current
+        # the argmax moves only with new round times or acceptance estimates: re-evaluated every `reeval` rounds (one
+        # heap expansion for every width; per round it cost ~5% of a 2-slot config-5 round in Python)
+        if self.best is None or self.rounds >= self._next_eval:
+            E = expected_iterations_upto(self.cands[-1], alphas, deltas)
+            self.best = max(self.cands, key=lambda k: E[k - 1] / self.time(k))
+            self._next_eval = self.rounds + self.reeval
+        if self.rounds % self.refresh == 0:                 # keep the neighbours' times current, alternately
             i = self.cands.index(self.best)
-            for j in (i - 1, i + 1):
-                if 0 <= j < len(self.cands):
-                    return self.cands[j]
+            j = i - 1 if (self.rounds // self.refresh) % 2 == 0 else i + 1
+            if not 0 <= j < len(self.cands):
+                j = i + 1 if j < i else i - 1
+            if 0 <= j < len(self.cands):
+                return self.cands[j]
         return self.best
 
     def record(self, k, seconds):

@@ -155,6 +155,8 @@ def test_expected_iterations_model():
     # a third branch for degenerate filters (probability d): the root, then its degenerate child (0.5), then 0.25
     assert pf.expected_iterations(3, [0.5], [0.5]) == pytest.approx(1.75)
     assert pf.expected_iterations(4, [0.3], [0.0]) == pytest.approx(pf.expected_iterations(4, [0.3]))
+    assert pf.expected_iterations_upto(6, [0.3, 0.7], [0.1, 0.0]) == pytest.approx(
+        [pf.expected_iterations(k, [0.3, 0.7], [0.1, 0.0]) for k in range(1, 7)])
 
 
 def test_slot_tuner_picks_the_best_measured_rate():
