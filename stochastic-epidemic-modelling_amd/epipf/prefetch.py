@@ -179,11 +179,12 @@ class SlotTuner:
     1.10e8 particle-steps/s, profiles/r4y_prefetch_cfg5.txt); the best and its neighbours re-measured every `refresh`
     rounds -- and E(K) comes from the chains' running acceptance rates."""
 
-    def __init__(self, lo, hi, tries=3, refresh=24, reeval=8):
+    def __init__(self, lo, hi, tries=3, refresh=24, reeval=8, prior=4):
         self.cands = sorted({lo} | {k for k in (1, 2, 4, 8, 16, 32, 64, 128) if lo <= k <= hi} | {hi})
         self.samples = {k: [] for k in self.cands}          # K -> the last round times (s)
         self.count = {k: 0 for k in self.cands}              # rounds run at K (the first is a warm-up)
-        self.tries, self.refresh, self.reeval = tries, refresh, reeval
+        self.yields = {k: [] for k in self.cands}           # K -> filters its last rounds committed
+        self.tries, self.refresh, self.reeval, self.prior = tries, refresh, reeval, prior
         self.rounds = 0
         self.best = None
         self._next_eval = 0
@@ -199,7 +200,7 @@ class SlotTuner:
         # heap expansion for every width; per round it cost ~5% of a 2-slot config-5 round in Python)
         if self.best is None or self.rounds >= self._next_eval:
             E = expected_iterations_upto(self.cands[-1], alphas, deltas)
-            self.best = max(self.cands, key=lambda k: E[k - 1] / self.time(k))
+            self.best = max(self.cands, key=lambda k: self.yield_of(k, E[k - 1]) / self.time(k))
             self._next_eval = self.rounds + self.reeval
         if self.rounds % self.refresh == 0:                 # keep the neighbours' times current, alternately
             i = self.cands.index(self.best)
@@ -210,10 +211,19 @@ class SlotTuner:
                 return self.cands[j]
         return self.best
 
-    def record(self, k, seconds):
+    def yield_of(self, k, model):
+        """Filters a round of K commits: the tree model's E(K) shrunk towards the rounds' observed yields (weight
+        `prior` rounds for the model).  The ideal tree overstates wide rounds (config 2, acceptance 0.08: E(32) /
+        E(16) = 1.28 modelled, 1.07 observed, so 32 slots were picked and ran 7-10% slower than 16)."""
+        obs = self.yields[k]
+        return (sum(obs) + self.prior * model) / (len(obs) + self.prior)
+
+    def record(self, k, seconds, committed=None):
         self.rounds += 1
         if k not in self.count:
             return
+        if committed is not None:
+            self.yields[k] = (self.yields[k] + [committed])[-16:]
         self.count[k] += 1
         if self.count[k] > 1:
             self.samples[k] = (self.samples[k] + [seconds])[-5:]
@@ -438,7 +448,7 @@ class PrefetchSampler(ChainSampler):
             self._evaluate(nodes)
         done = self._resolve()
         if self.tuner is not None and nodes:
-            self.tuner.record(self.slots, time.perf_counter() - t0)
+            self.tuner.record(self.slots, time.perf_counter() - t0, sum(self.filters_run) - f0)
         self.i = min(r.i for r in self.roots)
         if self.i >= self.iters:
             self._finish()
