@@ -129,6 +129,9 @@ static int pick_lanes(const epipf_ctx* c, int n_chains) {
     const long blocks = (long)n_chains * c->B, lb = c->lane_blocks;
     if (c->model == EPIPF_SIR || c->model == EPIPF_SEIR)
         return blocks <= lb / 4 ? 16 : blocks <= lb * 3 / 4 ? 8 : blocks <= lb ? 4 : 1;
+    // the W = 16 rule was measured on G = 2, whose decisions run as a fixed point (FastSubgroupsPacked::kFixedPoint,
+    // G <= 2); G = 3, 4 keep the sequential pass (W dependent decisions per chunk) and round 3's W = 8
+    if (c->G > 2) return blocks <= lb / 2 ? 8 : blocks <= lb ? 4 : 1;
     return blocks <= lb / 2 ? 16 : blocks <= lb ? 4 : 1;
 }
 
@@ -424,7 +427,12 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride; a.wstride = c->wstride; a.bstride = c->bstride;
     // S blocks per prefix segment: 1 (every block sum in LDS) for lane-group runs on 16-particle blocks up to
     // kMaxFlatGroupBlocks, else the smallest power of two with at most kMaxSegments segments
-    a.seg = (a.lanes > 1 && a.wg == kGroupBlock && a.B <= kMaxFlatGroupBlocks) ? 1 : prefix_segment(a.B);
+    // The 16-particle layout sums the step total in the 64-particle layout's order (scan_block_sums16): its segments are
+    // whole segments of that layout (S16 = 4 S64, the same as prefix_segment(B16) wherever it segments), and canon_per
+    // is that layout's 64-blocks per lane, so the log-likelihood is the same whichever layout the chain count picks.
+    const int B64 = (c->N + 63) / 64, S64 = prefix_segment(B64);
+    a.canon_per = ((B64 + S64 - 1) / S64 + 63) / 64 * S64;
+    a.seg = (a.lanes > 1 && a.wg == kGroupBlock) ? (a.B <= kMaxFlatGroupBlocks ? 1 : 4 * S64) : prefix_segment(a.B);
     a.nseg = (a.B + a.seg - 1) / a.seg;
     a.cert_k = cert_k(c->N, a.B, a.seg, 64);              // the block-sum scans run on 64 lanes whatever the layout
     // the reference-ambiguity test runs with the other device counters (bench.py's untimed counters iteration, the

@@ -4,7 +4,7 @@
 
 namespace epipf {
 
-size_t group_lds_bytes(int B, int S, int C, int W, int K) { return group_lds_bytes_impl(B, S, C, W, K); }
+size_t group_lds_bytes(int B, int S, int C, int W, int K, int PB) { return group_lds_bytes_impl(B, S, C, W, K, PB); }
 
 bool group_shape_supported(int W, int K) {
 #define EPIPF_HAS(w, k) if (W == w && K == k) return true;

@@ -518,10 +518,10 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
     }
 }
 
-// LDS of the lane-group step kernel: log table | tau exchange [W][K][64] | red[16] | particle rows [64][C] int32 |
-// block-sum prefix
-inline size_t group_lds_bytes_impl(int B, int S, int C, int W, int K) {
-    return step_lds_bytes_seg(B, S, 64) + sizeof(int32_t) * 64 * (size_t)C + sizeof(double) * 64 * (size_t)W * K;
+// LDS of the lane-group step kernel: log table | tau exchange [PB W / 64 waves][K][64] | red[16] | particle rows [64][C]
+// int32 | block-sum prefix.  PB particles per block (64 or kGroupBlock).
+inline size_t group_lds_bytes_impl(int B, int S, int C, int W, int K, int PB) {
+    return step_lds_bytes_seg(B, S, 64) + sizeof(int32_t) * 64 * (size_t)C + sizeof(double) * (size_t)PB * W * K;
 }
 
 // PB particles per block: 64 (the one-lane kernel's blocks), or kGroupBlock = 16 for runs that would leave CUs idle
@@ -536,8 +536,8 @@ __global__ __launch_bounds__(PB * W) void pf_step_group_kernel(StepArgs a, int p
     static_assert(PB * W >= 64 && (PB * W) % 64 == 0, "whole waves");
     extern __shared__ __attribute__((aligned(16))) double smem[];
     LogTab* tab = reinterpret_cast<LogTab*>(smem);
-    double* xch = smem + 2 * kLogTabEntries;             // the clock pass's tau exchange, [W waves][K][64]
-    double* red = xch + 64 * W * K;                      // [0]: the step's weight total, for every wave
+    double* xch = smem + 2 * kLogTabEntries;             // the clock pass's tau exchange, [PB W / 64 waves][K][64]
+    double* red = xch + PB * W * K;                      // [0]: the step's weight total, for every wave; [1]: scratch
     int32_t* rows = reinterpret_cast<int32_t*>(red + 16);
     double* seg_start = red + 16 + (64 * C + 1) / 2;
     double* seg_end = seg_start + a.nseg;
@@ -562,8 +562,12 @@ __global__ __launch_bounds__(PB * W) void pf_step_group_kernel(StepArgs a, int p
     if (wave == 0) {                                     // likelihood, resampling, gather: pf_step_kernel's code
         const int j = bp.b * PB + lane;
         const bool mine = lane < PB && j < a.N;
-        const double total = (a.seg == 1)
-                                 ? scan_block_sums<64, true>(a.bsum + bprev, a.B, seg_start + a.B, seg_start, red)
+        double total;
+        if constexpr (PB == kGroupBlock)                 // the total in the 64-particle layout's order (epipf_step.hpp)
+            total = scan_block_sums16<true>(a.bsum + bprev, a.B, a.canon_per, a.seg, seg_start + a.B, seg_start,
+                                            seg_start, seg_end, red + 1);
+        else
+            total = (a.seg == 1) ? scan_block_sums<64, true>(a.bsum + bprev, a.B, seg_start + a.B, seg_start, red)
                                  : scan_segments<true>(a.bsum + bprev, a.B, a.seg, a.nseg, seg_start, seg_end);
         if (lane == 0) red[0] = total;
         if (total > 0.0) {

@@ -44,6 +44,8 @@ struct StepArgs {
     int lane_events;              // pf_step_group_kernel: events per lane per chunk
     int xcd_map;                  // 1: 1-D grid of B x chains, each chain's blocks on one XCD (step_block); 0: 2-D grid
     int seg, nseg;                // block-sum prefix: S blocks per segment, ceil(B / S) segments (<= kMaxSegments)
+    int canon_per;                // 64-particle blocks per lane of the canonical total's scan (scan_block_sums16):
+                                  // the 64-layout's share, ceil(ceil(B64 / S64) / 64) S64, S64 = prefix_segment(B64)
     size_t hist_stride, anc_stride, wstride, bstride;
     double cert_k;                // K = N + 2D + 8 of the resampling certificate (epipf_device.hpp)
     double ref_k;                 // 2E (1 + 2^-10): reference-ambiguity bracket (ref_halfwidth)
@@ -182,7 +184,7 @@ size_t step_lds_bytes_seg(int B, int S, int wg);   // with S blocks per prefix s
 using GroupStepFn = void (*)(const StepArgs& a, int p, dim3 grid, size_t lds, hipStream_t s);
 GroupStepFn group_step_launcher(int model, int G, int obs, int W, int K);
 bool group_shape_supported(int W, int K);
-size_t group_lds_bytes(int B, int S, int C, int W, int K);
+size_t group_lds_bytes(int B, int S, int C, int W, int K, int PB);
 int prefix_segment(int B);
 constexpr int kMaxSegments = 200;
 // lane-group runs on 16-particle blocks keep every block sum and its prefix in LDS (S = 1) up to this many blocks

@@ -380,7 +380,7 @@ static hipError_t launch_filter_t(const StepArgs& a, int n_chains, const FilterS
     // W lanes per particle (runs too small to fill the chip): the lane-group step kernel, epipf_group.hip
     const GroupStepFn group = a.lanes > 1 ? group_step_launcher(MODEL, G, OBS, a.lanes, a.lane_events) : nullptr;
     if (a.lanes > 1 && !group) return hipErrorInvalidValue;
-    const size_t glds = group ? group_lds_bytes(a.B, a.seg, C, a.lanes, a.lane_events) : 0;
+    const size_t glds = group ? group_lds_bytes(a.B, a.seg, C, a.lanes, a.lane_events, a.wg) : 0;
     for (int g = 0; g < S; ++g) {
         StepArgs ag = a;
         ag.chain0 = (int)((long)n_chains * g / S);

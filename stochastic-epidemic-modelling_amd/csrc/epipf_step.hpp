@@ -93,4 +93,55 @@ __device__ __forceinline__ double scan_segments(const double* __restrict__ bsum_
     return seg_end[nseg - 1];
 }
 
+// The block-sum prefix of a run on 16-particle blocks (lane-group runs, kGroupBlock), with the step's TOTAL summed in
+// the 64-particle layout's order, so that a filter's log-likelihood does not depend on which layout its launch used
+// (the layout follows the number of chains sharing the launch, pick_block).  The 64-layout total is
+//   c_m = the in-block scan's last lane over 64-block m = (s_4m + s_4m+1) + (s_4m+2 + s_4m+3)
+// exactly: block_inclusive_scan's Hillis-Steele window at lane 63 is the balanced tree of its four aligned 16-lane
+// windows, each the 16-particle block's own scan result s (lane 15, the lanes past the block adding nothing), and
+// IEEE addition commutes; then lane l adds the c_m of its P consecutive 64-blocks in order (P = a.canon_per: the
+// 64-layout's per-lane share, scan_block_sums / scan_segments), a wave scan gives each lane its offset, and the total is
+// the last lane's running sum.  Blocks past N hold weights 0 in both layouts (sums exact).
+// Outputs for the 16-particle search: flat (S16 = 1) every block's exclusive prefix and sum (bpex, bsum); segmented
+// (S16 = 4 S64, whole 64-blocks per segment) seg_start / seg_end.  Inside a 64-block the 16-block prefixes are
+// e, e + s0, e + (s0 + s1), e + ((s0 + s1) + s2): other roundings of the same prefixes, within the resampling
+// certificate's depth bound (cert_k is taken on the 16-block layout's larger D), so the search stays certified.
+// The total goes through LDS (*tot, written by the lane holding the last 64-block).
+template <bool WAVE>
+__device__ __forceinline__ double scan_block_sums16(const double* __restrict__ bsum_g, int B16, int P, int S16,
+                                                    double* bpex, double* bsum, double* seg_start, double* seg_end,
+                                                    double* tot) {
+    const int lane = threadIdx.x & 63;
+    const int B64 = (B16 + 3) >> 2;
+    const int m0 = min(lane * P, B64), m1 = min(m0 + P, B64);
+    auto sub = [&](int i) __attribute__((always_inline)) { return i < B16 ? bsum_g[i] : 0.0; };
+    double s = 0.0;
+    for (int m = m0; m < m1; ++m) {
+        const double s0 = sub(4 * m), s1 = sub(4 * m + 1), s2 = sub(4 * m + 2), s3 = sub(4 * m + 3);
+        s = s + ((s0 + s1) + (s2 + s3));
+    }
+    const double inc = block_inclusive_scan<64>(s, nullptr);
+    const double up = __shfl_up(inc, 1, 64);
+    double e = (lane == 0) ? 0.0 : up;
+    for (int m = m0; m < m1; ++m) {
+        const int i = 4 * m;
+        const double s0 = sub(i), s1 = sub(i + 1), s2 = sub(i + 2), s3 = sub(i + 3);
+        const double s01 = s0 + s1;
+        if (S16 == 1) {
+            bpex[i] = e;
+            bsum[i] = s0;
+            if (i + 1 < B16) { bpex[i + 1] = e + s0; bsum[i + 1] = s1; }
+            if (i + 2 < B16) { bpex[i + 2] = e + s01; bsum[i + 2] = s2; }
+            if (i + 3 < B16) { bpex[i + 3] = e + (s01 + s2); bsum[i + 3] = s3; }
+        } else if (i % S16 == 0) {
+            seg_start[i / S16] = e;
+        }
+        e = e + (s01 + (s2 + s3));
+        if (S16 > 1 && ((i + 4) % S16 == 0 || m == B64 - 1)) seg_end[i / S16] = e;
+        if (m == B64 - 1) *tot = e;
+    }
+    lds_sync<WAVE>();
+    return *tot;
+}
+
 }  // namespace epipf

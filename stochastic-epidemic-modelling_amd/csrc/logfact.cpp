@@ -65,15 +65,24 @@ void logfact_table(int n_max, double* out) {
         fill_threaded(0, n, out, lo);
         return;
     }
-    std::lock_guard<std::mutex> lock(g_lf_mu);
-    const int have = (int)g_lf_hi.size();
-    if (have < n) {
-        g_lf_hi.resize(n);
-        g_lf_lo.resize(n);
-        fill_threaded(have, n, g_lf_hi.data(), g_lf_lo.data());
+    // the lock covers the copies only: the missing entries (seconds for millions of them) are computed outside it, so
+    // other contexts' set_population calls are not held behind a long fill; entries depend on n alone, so concurrent
+    // fills of the same range write the same values and whichever extends the cache first wins
+    int have;
+    {
+        std::lock_guard<std::mutex> lock(g_lf_mu);
+        have = std::min((int)g_lf_hi.size(), n);
+        std::copy(g_lf_hi.begin(), g_lf_hi.begin() + have, out);
+        std::copy(g_lf_lo.begin(), g_lf_lo.begin() + have, lo);
     }
-    std::copy(g_lf_hi.begin(), g_lf_hi.begin() + n, out);
-    std::copy(g_lf_lo.begin(), g_lf_lo.begin() + n, lo);
+    if (have == n) return;
+    fill_threaded(have, n, out, lo);
+    std::lock_guard<std::mutex> lock(g_lf_mu);
+    const int cur = (int)g_lf_hi.size();
+    if (cur < n) {
+        g_lf_hi.insert(g_lf_hi.end(), out + cur, out + n);
+        g_lf_lo.insert(g_lf_lo.end(), lo + cur, lo + n);
+    }
 }
 
 // hi/lo of log(p) and log1p(-p) (the weight's per-chain constants)

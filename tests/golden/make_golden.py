@@ -106,7 +106,9 @@ class _RandomProxy:
         return _INJ.choice(a, size, replace, p)
 
     def uniform(self, low=0.0, high=1.0, size=None):
-        assert S.abc and size is None
+        if not S.abc:  # MH acceptance uniform (pmcmc.py:395): numpy's real global RandomState
+            return np.random.uniform(low, high, size)
+        assert size is None
         c = S.abc_uniforms
         S.abc_uniforms += 1
         S.t = c // 2  # abc_algo.py:35-36: beta then gamma, one trial per pair
@@ -484,8 +486,24 @@ PMCMC_CASES = [
 ]
 
 
-def run_pmcmc_cases(pm, d, out):
-    for name, model, ds, rows, params, h, sigma, iters, probs, N, npop, mu, adaptive, seed, key in PMCMC_CASES:
+# BASELINE-shape traces, one file per case so the two can be generated in parallel processes:
+#  * cfg1_full: BASELINE configs[0] literally -- SIR, N=100, pop 200, T=50 (the cfg1 ODE recipe), h=.01, Sigma=I,
+#    500 MH iterations, probs=.1;
+#  * test_pmcmc_p: the shape of the reference's own tests/test_pmcmc_p.py:40-61 -- sir_binom (its commented
+#    data recipe :21-29), N=100, pop 4820, T=15, probs=None (p is the third parameter), h=5, the Sigma of :40-44;
+#    the start theta is (2, 1, .1) because the run's thetas.csv (:34-38) is not in the reference checkout.
+TEST_PMCMC_P_SIGMA = np.array([[8.56210710e-03, 4.96880438e-03, -2.94152350e-05],
+                               [4.96880438e-03, 3.20130528e-03, -1.73813239e-05],
+                               [-2.94152350e-05, -1.73813239e-05, 2.68921978e-06]])
+PMCMC_BASELINE_CASES = [
+    ("cfg1_full", "SIR", "cfg1_binom", None, [2.0, 1.0], 0.01, None, 500, 0.1, 100, 200, 20, False, 101, 2101),
+    ("test_pmcmc_p", "SIR", "sir_binom", None, [2.0, 1.0, 0.1], 5.0, TEST_PMCMC_P_SIGMA, 40, None, 100, 4820, 20,
+     False, 102, 2102),
+]
+
+
+def run_pmcmc_cases(pm, d, out, cases=PMCMC_CASES):
+    for name, model, ds, rows, params, h, sigma, iters, probs, N, npop, mu, adaptive, seed, key in cases:
         Y = d[ds] if rows is None else d[ds][:rows]
         S.key = key
         S.next_f = 0
@@ -528,13 +546,14 @@ def main():
 
     check_numpy_identities()
     d = make_datasets(pm)
-    np.savez_compressed(os.path.join(HERE, "datasets.npz"), **d)
-    data_dir = os.path.join(REPO, "stochastic-epidemic-modelling_amd", "epipf", "data")
-    os.makedirs(data_dir, exist_ok=True)
-    np.savetxt(os.path.join(data_dir, "sir_subgrps.csv"), d["cfg5_ssa"], delimiter=", ")   # :78
+    only = set(args.only.split(",")) if args.only else None
+    if not only:  # --only runs leave the committed dataset files untouched
+        np.savez_compressed(os.path.join(HERE, "datasets.npz"), **d)
+        data_dir = os.path.join(REPO, "stochastic-epidemic-modelling_amd", "epipf", "data")
+        os.makedirs(data_dir, exist_ok=True)
+        np.savetxt(os.path.join(data_dir, "sir_subgrps.csv"), d["cfg5_ssa"], delimiter=", ")   # :78
     pf = install_shim(pm, ga)
     ab.np = pm.np
-    only = set(args.only.split(",")) if args.only else None
     if not only or "filter" in only:
         out = {}
         run_filter_cases(pm, pf, d, out)
@@ -557,6 +576,11 @@ def main():
         out = {}
         run_abc_cases(ab, d, out)
         save(out, os.path.join(HERE, "abc_golden.npz"))
+    for case in PMCMC_BASELINE_CASES:  # minutes each: only when named (--only cfg1_full / test_pmcmc_p)
+        if only and case[0] in only:
+            out = {}
+            run_pmcmc_cases(pm, d, out, [case])
+            save(out, os.path.join(HERE, f"pmcmc_{case[0]}_golden.npz"))
 
 
 if __name__ == "__main__":

@@ -3,6 +3,7 @@ compute calls, no device needed)."""
 import ctypes
 import os
 import re
+import subprocess
 
 import pytest
 
@@ -65,10 +66,20 @@ def test_constants_match_header():
     assert int(defs["EPIPF_PROFILE_COUNTERS"]) == _lib.PROFILE_COUNTERS
 
 
-def test_build_id_is_a_source_hash():
+def makefile_build_id():
+    """The id csrc/Makefile stamps into the libraries: sha256 of the exact source, header, script and Makefile list
+    it names (csrc/Makefile BUILD_ID), evaluated by make itself."""
+    out = subprocess.run(["make", "-s", "--no-print-directory", "-C", os.path.join(PKG, "csrc"), "build-id"],
+                         check=True, capture_output=True, text=True).stdout.strip()
+    assert len(out) == 16 and int(out, 16) >= 0, out
+    return out
+
+
+def test_build_id_matches_the_sources():
+    """The loaded libepipf.so was built from the sources in this tree: a stale prebuilt library (pushed to the GPU box
+    next to edited sources) fails here, and with it every PMC profile bench.py would match on its id."""
     from epipf import _lib
-    bid = _lib.build_id()
-    assert len(bid) == 16 and int(bid, 16) >= 0, bid
+    assert _lib.build_id() == makefile_build_id(), "libepipf.so is stale: rebuild (__graft_entry__.build())"
 
 
 def test_debug_library_exports_the_same_boundary():
@@ -79,4 +90,4 @@ def test_debug_library_exports_the_same_boundary():
     assert not [s for s in declared_symbols() if not hasattr(D, s)]
     D.epipf_build_id.restype = ctypes.c_char_p
     from epipf import _lib
-    assert D.epipf_build_id().decode() == _lib.build_id() + "-debug"
+    assert D.epipf_build_id().decode() == makefile_build_id() + "-debug", "libepipf_debug.so is stale"

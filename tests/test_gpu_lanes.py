@@ -140,9 +140,8 @@ def test_lane_groups_larger_subgroup_models_equal_one_lane(datasets_golden, G):
         assert int(got[1][0]) == int(ref[1][0])
         np.testing.assert_array_equal(got[2], ref[2])
         np.testing.assert_array_equal(got[3], ref[3])
-        # equal bit for bit on the same weight layout; with 16-particle blocks (EPIPF_GROUP_BLOCK=16) the step totals
-        # are summed over another tree, an ulp apart -- the oracle comparisons' bar
-        np.testing.assert_allclose(got[0], ref[0], rtol=1e-12, atol=1e-9)
+        # bit for bit: the 16-particle layout sums the step totals in the 64-particle layout's order
+        np.testing.assert_array_equal(got[0], ref[0])
 
 
 @pytest.mark.parametrize("lanes", [2, 16])
@@ -291,3 +290,67 @@ def test_certified_clock_redo_equals_oracle(datasets_golden, monkeypatch, model,
         np.testing.assert_array_equal(hid[ch], o["hidden"])
         np.testing.assert_array_equal(anc[ch], o["ancestry"])
         np.testing.assert_allclose(lz[ch], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
+def _run_layout(monkeypatch, model, c, N, chains, lanes, block, keys, fidx):
+    """_run on a context created with EPIPF_GROUP_BLOCK=block (read at create: 16- or 64-particle weight blocks)."""
+    monkeypatch.setenv("EPIPF_GROUP_BLOCK", str(block))
+    try:
+        return _run(model, c, N, chains, lanes, keys, fidx)
+    finally:
+        monkeypatch.delenv("EPIPF_GROUP_BLOCK")
+
+
+@pytest.mark.parametrize("N", [10000, 12865, 25000])
+def test_step_totals_do_not_depend_on_the_weight_layout(datasets_golden, monkeypatch, N):
+    """the weight layout (16- or 64-particle blocks) follows the number of chains sharing a launch, so a
+    filter's log-likelihood must not depend on it.  The 16-particle layout sums each step's total in the 64-particle
+    layout's order (scan_block_sums16): one lane per particle, W = 8 and 16 on either layout, one and eight chains --
+    log-likelihoods bit-identical, states and ancestors the oracle's.  N = 10^4 (157 / 625 blocks, flat prefix),
+    12865 (202 64-blocks: a segmented 64-layout prefix, S = 2), 25000 (1563 16-blocks: the segmented 16-layout)."""
+    c = dict(_case(datasets_golden, "sir"))
+    c["Y"] = datasets_golden["sir_binom"][:6]
+    ref = _run("sir", c, N, 1, 1, [91], [4])
+    runs = [_run_layout(monkeypatch, "sir", c, N, 1, W, blk, [91], [4]) for W in (8, 16) for blk in (16, 64)]
+    eight = _run_layout(monkeypatch, "sir", c, N, 8, 16, 16, [91] + list(range(92, 99)), [4] * 8)
+    for got in runs + [eight]:
+        assert int(got[1][0]) == int(ref[1][0]) == 0
+        np.testing.assert_array_equal(got[0][0], ref[0][0])
+        np.testing.assert_array_equal(got[2][0], ref[2][0])
+        np.testing.assert_array_equal(got[3][0], ref[3][0])
+    o = oracle.particle_filter(c["Y"], "sir", c["theta"], False, 0.1, N, c["npop"], c["mu"], key=91, filter_index=4)
+    np.testing.assert_array_equal(ref[2][0], o["hidden"])
+    np.testing.assert_array_equal(ref[3][0], o["ancestry"])
+    np.testing.assert_allclose(ref[0][0], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
+def test_subgroup_totals_do_not_depend_on_the_weight_layout(datasets_golden, monkeypatch):
+    """The same for the 2-group model at N = 10^4 (W = 16 on 16-particle blocks, its automatic one-chain layout)."""
+    c = _case(datasets_golden, "sir_subgroups")
+    c["Y"] = c["Y"][:5]
+    ref = _run("sir_subgroups", c, 10000, 1, 1, [93], [1])
+    for blk in (16, 64):
+        got = _run_layout(monkeypatch, "sir_subgroups", c, 10000, 1, 16, blk, [93], [1])
+        np.testing.assert_array_equal(got[0], ref[0])
+        np.testing.assert_array_equal(got[2], ref[2])
+        np.testing.assert_array_equal(got[3], ref[3])
+
+
+def test_prefetch_widths_and_chain_counts_agree_at_ten_thousand_particles(datasets_golden):
+    """ADVICE r4's case: at N = 10^4 speculative rounds of 2 and 16 slots (W = 16 on 16-particle blocks vs W = 8 / 4 on
+    64-particle blocks) and a lone chain vs the same chain among eight give bit-identical log-likelihoods, thetas and
+    trajectories."""
+    from epipf.pmcmc import ChainSampler, chain_key
+    from epipf.prefetch import PrefetchSampler
+    Y = datasets_golden["cfg2_binom"][:40]
+    kw = dict(iters=12, probs=0.1, n_particles=10000, n_population=10000.0, mu=20.0, mh_ratio="log")
+    res = []
+    for cls, chains, extra in ((PrefetchSampler, 1, {"slots": 2}), (PrefetchSampler, 1, {"slots": 16}),
+                               (ChainSampler, 1, {}), (ChainSampler, 8, {})):
+        rngs = [np.random.RandomState(70 + c) for c in range(chains)]
+        s = cls(Y, "sir", [0.25, 0.1], 2e-4, **kw, rngs=rngs, keys=[chain_key(70, c) for c in range(chains)], **extra)
+        res.append(s.run()[0])
+    for r in res[1:]:
+        np.testing.assert_array_equal(r.log_likelihoods, res[0].log_likelihoods)
+        np.testing.assert_array_equal(r.thetas, res[0].thetas)
+        np.testing.assert_array_equal(r.sampled_trajs, res[0].sampled_trajs)
