@@ -11,9 +11,10 @@ all-gathered over RCCL at the end of the timed region (pmcmc chain gather, SURVE
 
 Also reported: roofline of the dominant kernel (pf_step_kernel, HIP-event timed on the engine's stream),
 a CPU baseline (the oracle C restatement, OpenMP, on a bounded sample) on rank 0 at N=1, and `configs`: short
-timed runs of the other BASELINE workloads -- configs 3, 4, 5 at 256 chains per GPU and config 5 at ONE chain per GPU
-(BASELINE's "8 independent chains across 8 GPUs" layout, the lane-group kernel) -- each with its own roofline where a
-PMC profile of that (config, chains, lanes) on this library build is committed (profiles/pmc_*.json).
+timed runs of the other BASELINE workloads -- configs 1, 3, 4, 5 at 256 chains per GPU and config 5 at ONE chain per
+GPU (BASELINE's "8 independent chains across 8 GPUs" layout, the lane-group kernel) -- each with its own roofline where
+a PMC profile of that (config, chains, lanes) on this library build is committed (profiles/pmc_*.json), and its own
+CPU baseline with the reference-calibrated rate of that config (profiles/reference_timing_cfg<c>.json).
 """
 import argparse
 import glob
@@ -32,7 +33,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters
 VALU_PEAK = 1024 * 2.4e9 / 2   # wave64 VALU instructions/s: 1024 SIMDs, 2.4 GHz, one wave64 instruction per 2 cycles
 MODEL_NAMES = {"sir": "SIR", "seir": "SEIR", "sir_subgroups": "multi-subgroup SIR", "sir_subgroups2": "SIR subgroups2"}
 # the `configs` workloads: name -> (BASELINE config, chains per GPU)
-CONFIG_RUNS = {"3": (3, 256), "4": (4, 256), "5": (5, 256), "5x1": (5, 1)}
+CONFIG_RUNS = {"1": (1, 256), "3": (3, 256), "4": (4, 256), "5": (5, 256), "5x1": (5, 1)}
 
 
 def parse():
@@ -52,10 +53,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--single-chain", action=argparse.BooleanOptionalAction, default=True,
                     help="also time 1 chain/GPU (N=1 only): one filter per MH iteration, and speculative MH (extra fields)")
-    ap.add_argument("--configs", default="3,4,5,5x1",
+    ap.add_argument("--configs", default="1,3,4,5,5x1",
                     help="extra timed workloads for the `configs` object (comma list of " + ", ".join(CONFIG_RUNS) +
                          "; 'none' to skip)")
     ap.add_argument("--configs-steps", type=int, default=4, help="timed MH iterations per `configs` workload")
+    ap.add_argument("--configs-cpu-seconds", type=float, default=3.0,
+                    help="CPU baseline per `configs` workload: seconds of port filters at 1 thread and at all threads")
     ap.add_argument("--pipelines", type=int, default=int(os.environ.get("EPIPF_BENCH_PIPELINES", 0)),
                     help="chain groups on their own engine + host thread, so each group's MH host work overlaps the "
                          "others' filters (epipf.pmcmc.run_pipelined); 1 = one lockstep sampler; 0 = automatic: 2 "
@@ -88,12 +91,22 @@ def host_threads():
     return max(1, min(avail, int(env))) if env and env.isdigit() else avail
 
 
-def cpu_baseline(Y, meta, N, seconds):
+def reference_calibration(cfg):
+    """The port/reference factors scripts/time_reference.py measured for BASELINE config `cfg` in the build container
+    (the unmodified reference's particle_filter at jobs=1 / jobs=-1 next to the port on the same data), or None."""
+    path = os.path.join(REPO, "profiles", f"reference_timing_cfg{cfg}.json")
+    if not os.path.exists(path):
+        return None, None
+    return json.load(open(path)), os.path.relpath(path, REPO)
+
+
+def cpu_baseline(Y, meta, N, seconds, cfg):
     """The oracle (C restatement of the reference filter, OpenMP over particles) on the GPU box's host, at 1 thread
-    and at every thread this process is allotted.  Sample: whole filters of the bench config (N particles x T
-    steps) repeated until `seconds` elapse (at least one) per thread count.  The reference itself never runs on the
-    GPU box: scripts/time_reference.py times it in the build container next to the same port, and the
-    port/reference factor it measured (profiles/r2_reference_timing.json) converts the port's rates into the
+    and at every thread this process is allotted.  Sample: whole filters of N particles x T steps of the config's data
+    (the bench config's N; the `configs` entries a capped N, the rate per particle-step not depending on N) repeated
+    until `seconds` elapse (at least one) per thread count.  The reference itself never runs on the GPU box:
+    scripts/time_reference.py times it in the build container next to the same port, per config, and the
+    port/reference factor it measured (profiles/reference_timing_cfg<c>.json) converts the port's rates into the
     reference's (`reference_calibrated`)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
@@ -122,22 +135,24 @@ def cpu_baseline(Y, meta, N, seconds):
     n1, dt1, ev1, _ = timed(1, seconds)
     value, value1 = n * N * Y.shape[0] / dt, n1 * N * Y.shape[0] / dt1
     base = dict(value=value, unit="particle-steps/s", cores=used, kind="port",
-                sample=f"{n} full filter(s) of the bench config (N={N}, T={Y.shape[0]}) on {used} threads in {dt:.1f}s "
+                sample=f"{n} full filter(s) of config {cfg} (N={N}, T={Y.shape[0]}) on {used} threads in {dt:.1f}s "
                        f"({ev / dt:.3g} events/s); host CPU: {cpu_model()}, {used} threads allotted to this process of "
                        f"{os.cpu_count()} on the machine",
                 single_core={"value": value1, "cores": 1, "sample": f"{n1} full filter(s) in {dt1:.1f}s",
                              "events_per_s": ev1 / dt1})
-    cal_path = os.path.join(REPO, "profiles", "r2_reference_timing.json")
-    if os.path.exists(cal_path) and meta["model"] == "sir":
-        cal = json.load(open(cal_path))
-        f1 = cal["factor_port_over_reference_1core"]
+    cal, cal_path = reference_calibration(cfg)
+    if cal:
+        f1, fall = cal["factor_port_over_reference_1core"], cal["factor_port_over_reference_allcores"]
         base["reference_calibrated"] = {
             "reference_1core_value": value1 / f1,
+            "reference_allcores_value": value / fall,
             "factor_port_over_reference_1core": f1,
+            "factor_port_over_reference_allcores": fall,
             "reference_measured": {k: v["particle_steps_per_s"] for k, v in cal["reference"].items()},
+            "reference_events_per_particle_step": cal.get("reference_events_per_particle_step"),
             "reference_host": f"{cal['host_cpu']} ({cal['host_cpus']} CPUs), build container",
-            "source": "profiles/r2_reference_timing.json (scripts/time_reference.py: unmodified reference "
-                      "particle_filter, jobs=1 / jobs=-1, config 2 data)"}
+            "source": f"{cal_path} (scripts/time_reference.py: unmodified reference particle_filter, jobs=1 / "
+                      f"jobs=-1, config {cfg} data)"}
     return base
 
 
@@ -423,19 +438,27 @@ def config_runs(ctx, args):
     fixed_theta where that differs."""
     names = [] if args.configs.strip().lower() in ("", "none") else [c.strip() for c in args.configs.split(",")]
     out = {}
+    cpu_done = {}
     for name in names:
         if name not in CONFIG_RUNS:
             raise SystemExit(f"bench.py: unknown --configs entry {name!r}")
         cfg, chains = CONFIG_RUNS[name]
         steps = args.configs_steps * (5 if chains == 1 else 1)        # one-chain MH iterations are short
+        from epipf import datasets
+        Yc, mc = datasets.benchmark_dataset(cfg)
+        # host-bound MH steps (config 1: N x T = 5,000 per filter): two chain groups' host work overlaps (main())
+        pipelines = 2 if chains > 1 and mc["N"] * Yc.shape[0] <= 20000 else 1
+        if cfg == 1:
+            steps *= 10                                                # 2-3 ms MH steps: time a few hundred ms
         entry = None
         for kind in ("config", "fixed_theta"):
-            run = timed_chains(ctx, args, cfg, chains, steps, 1 if chains > 1 else 2, kind)
+            run = timed_chains(ctx, args, cfg, chains, steps, 1 if chains > 1 else 2, kind, pipelines=pipelines)
             run["cfg"] = cfg
             if entry is None:
                 entry = run_summary(run)
                 entry["workload"] = (f"BASELINE config {cfg}: {run['meta']['model'].upper()} PMCMC, N={run['N']}, "
                                      f"T={run['T']}, {chains} chain(s) per GPU")
+                entry["pipelines"] = run["P"]
                 entry["roofline"] = roofline(run, run["value"])
                 if run["proposal"] == proposal(run["meta"], "fixed_theta")[2]:
                     entry["proposal_kind"] = "fixed_theta (the config has no reference proposal)"
@@ -446,6 +469,17 @@ def config_runs(ctx, args):
         if chains == 1 and ctx.rank == 0 and ctx.world == 1:
             entry["prefetch_auto"] = prefetch_chain(args, run["Y"], run["meta"], run["N"], run["T"], ctx.local, "auto",
                                                     160, h=entry["h"], sigma=run["meta"]["sigma"])
+        if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline and args.configs_cpu_seconds > 0 \
+                and name not in cpu_done:
+            # the same CPU baseline as the headline's, per config, on a capped particle count
+            cpu_done[name] = cpu_baseline(run["Y"], run["meta"], min(run["N"], 2048), args.configs_cpu_seconds, cfg)
+        if name in cpu_done:
+            entry["cpu_baseline"] = cpu_done[name]
+            entry["speedup_vs_cpu_baseline"] = entry["value"] / cpu_done[name]["value"]
+            rc = cpu_done[name].get("reference_calibrated")
+            if rc:
+                entry["speedup_vs_reference_1core_calibrated"] = entry["value"] / rc["reference_1core_value"]
+                entry["speedup_vs_reference_allcores_calibrated"] = entry["value"] / rc["reference_allcores_value"]
         out[name] = entry
     return out
 
@@ -536,7 +570,7 @@ def main():
 
     base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        base = cpu_baseline(Y, meta, N, args.cpu_baseline_seconds)
+        base = cpu_baseline(Y, meta, N, args.cpu_baseline_seconds, args.config)
 
     if rank == 0:
         # distinct GPUs, not ranks: (host, device) pairs over all ranks (gloo rehearsals put several ranks on one)
@@ -597,6 +631,8 @@ def main():
             line["speedup_vs_cpu_single_core"] = value / base["single_core"]["value"]
             if "reference_calibrated" in base:
                 line["speedup_vs_reference_1core_calibrated"] = value / base["reference_calibrated"]["reference_1core_value"]
+                line["speedup_vs_reference_allcores_calibrated"] = \
+                    value / base["reference_calibrated"]["reference_allcores_value"]
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

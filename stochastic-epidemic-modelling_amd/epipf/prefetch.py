@@ -169,22 +169,29 @@ def expected_iterations(slots, alphas, deltas=None):
 
 
 class SlotTuner:
-    """slots="auto": the round width that maximises committed iterations per second of wall time.  A round's
+    """slots="auto": the round width that maximises committed filters per second of wall time.  A round's
     wall time T(K) grows with its K filters once they no longer fit the idle SIMDs (the lane-group kernel and
-    the chip's fill set where), and its yield E(K) (expected_iterations) grows sub-linearly at a rate set by the
-    acceptance rate, so the best K depends on both; T(K) is measured on the chain's own rounds -- each candidate power
-    of two run once to warm up (not timed: a first launch shape pays one-off costs) and then `tries` times, T(K) the
-    median of its last five rounds (a round lasts as long as its slowest filter, and the filters' costs vary with their
-    theta: at config 5's h = 1 a fastest-of-three estimate picked 4 slots in one run and 1 in another, 0.78e8 against
-    1.10e8 particle-steps/s, profiles/r4y_prefetch_cfg5.txt); the best and its neighbours re-measured every `refresh`
-    rounds -- and E(K) comes from the chains' running acceptance rates."""
+    the chip's fill set where), and its yield E(K) grows sub-linearly at a rate set by the acceptance rate, so the best
+    K depends on both.  T(K) is measured on the chain's own rounds -- each candidate power of two run once to warm up
+    (not timed: a first launch shape pays one-off costs) and then `tries` times, T(K) the median of its last five rounds
+    (a round lasts as long as its slowest filter, and the filters' costs vary with their theta: at config 5's h = 1 a
+    fastest-of-three estimate picked 4 slots in one run and 1 in another, profiles/r4y_prefetch_cfg5.txt); the best and
+    its neighbours re-measured every `refresh` rounds.
+    E(K) is OBSERVED, not modelled: the scheduler is best-first, so the K' < K most probable nodes of a K-slot round are
+    exactly what a K'-slot round would have run from the same root, and a round at width K therefore also tells what
+    every narrower width would have committed (PrefetchSampler._resolve: the realised path cut at its first node of
+    schedule rank >= K').  Every round adds one sample to each width up to its own; the tree model
+    (expected_iterations, independent accept / reject at the running rates) only seeds the estimate while samples are
+    few (weight `prior` rounds) -- on its own it overstated wide rounds (config 2, acceptance 0.08: E(32) / E(16) = 1.28
+    modelled, 1.07 observed, so 32 slots were picked and ran 10% slower than 16, BENCH_r04)."""
 
-    def __init__(self, lo, hi, tries=3, refresh=24, reeval=8, prior=4):
+    def __init__(self, lo, hi, tries=3, refresh=24, reeval=8, prior=2, window=64):
         self.cands = sorted({lo} | {k for k in (1, 2, 4, 8, 16, 32, 64, 128) if lo <= k <= hi} | {hi})
         self.samples = {k: [] for k in self.cands}          # K -> the last round times (s)
         self.count = {k: 0 for k in self.cands}              # rounds run at K (the first is a warm-up)
-        self.yields = {k: [] for k in self.cands}           # K -> filters its last rounds committed
-        self.tries, self.refresh, self.reeval, self.prior = tries, refresh, reeval, prior
+        self.yields = {k: [] for k in self.cands}           # K -> filters a K-slot round committed (observed or
+                                                             # cut from a wider round), the last `window`
+        self.tries, self.refresh, self.reeval, self.prior, self.window = tries, refresh, reeval, prior, window
         self.rounds = 0
         self.best = None
         self._next_eval = 0
@@ -212,18 +219,22 @@ class SlotTuner:
         return self.best
 
     def yield_of(self, k, model):
-        """Filters a round of K commits: the tree model's E(K) shrunk towards the rounds' observed yields (weight
-        `prior` rounds for the model).  The ideal tree overstates wide rounds (config 2, acceptance 0.08: E(32) /
-        E(16) = 1.28 modelled, 1.07 observed, so 32 slots were picked and ran 7-10% slower than 16)."""
+        """Filters a round of K commits: the mean of the observed yields of width K (its own rounds and the cuts of
+        wider ones), the tree model's E(K) counting as `prior` rounds."""
         obs = self.yields[k]
         return (sum(obs) + self.prior * model) / (len(obs) + self.prior)
 
     def record(self, k, seconds, committed=None):
+        """A round of width k took `seconds`; committed: {K': filters a K'-slot round would have committed} for the
+        candidates K' <= k (PrefetchSampler._resolve), or the round's own count."""
         self.rounds += 1
+        if committed is not None:
+            cuts = committed if isinstance(committed, dict) else {k: committed}
+            for kk, v in cuts.items():
+                if kk in self.yields:
+                    self.yields[kk] = (self.yields[kk] + [v])[-self.window:]
         if k not in self.count:
             return
-        if committed is not None:
-            self.yields[k] = (self.yields[k] + [committed])[-16:]
         self.count[k] += 1
         if self.count[k] > 1:
             self.samples[k] = (self.samples[k] + [seconds])[-5:]
@@ -254,6 +265,7 @@ class PrefetchSampler(ChainSampler):
         self.speculative_filters = 0
         self.degenerate = 0                                     # realised filters that returned (None, None, None)
         self.degenerate_c = [0] * self.nc                       # the same per chain (the scheduler's third branch)
+        self._rank = {}
 
     # ------------------------------------------------------------------ host draws
     def _factor(self, std):
@@ -380,6 +392,7 @@ class PrefetchSampler(ChainSampler):
         tr = self.eng.path_sample(chosen) if np.any(st == _lib.STATUS_OK) else None
         for s, x in enumerate(nodes):
             x.result = (lz[s].copy(), int(st[s]), None if tr is None else tr[s])
+        self._rank = {id(x): s for s, x in enumerate(nodes)}    # this round's schedule ranks (best-first order)
         self.last_active = n
         self.speculative_filters += n
         self.rounds += 1
@@ -402,11 +415,16 @@ class PrefetchSampler(ChainSampler):
         if accepted:
             self.acceptances[c] += 1
 
-    def _resolve(self):
-        """Walk every chain's realised path as far as the evaluated filters reach; returns iterations committed."""
+    def _resolve(self, widths=()):
+        """Walk every chain's realised path as far as the evaluated filters reach; returns (iterations committed,
+        {K': realised-path filters a K'-slot round would have committed} for K' in widths).  The cut for K' ends each
+        chain's walk at its first filter of this round's schedule rank >= K' (best-first: a K'-slot round runs the same
+        first K' nodes)."""
         done = 0
+        cut = dict.fromkeys(widths, 0)
         for c in range(self.nc):
             x = self.roots[c]
+            nf, first = 0, {}                                    # filters walked; width -> filters before its cut
             while x.i < self.iters:
                 self._expand(x)
                 if x.neg:
@@ -415,16 +433,23 @@ class PrefetchSampler(ChainSampler):
                 elif x.result is None:
                     break
                 else:
+                    r = self._rank.get(id(x), -1)                # -1: evaluated in an earlier round
+                    for kk in widths:
+                        if kk not in first and r >= kk:
+                            first[kk] = nf
                     y = self._decision(x)
                     ok = x.result[1] == _lib.STATUS_OK
                     self.degenerate += 0 if ok else 1
                     self.degenerate_c[c] += 0 if ok else 1
                     self._commit(c, x, y, True, ok and y is x.kids[0])
+                    nf += 1
                 x = y
                 done += 1
+            for kk in widths:
+                cut[kk] += first.get(kk, nf)
             x.parent = None                                      # drop the discarded tree
             self.roots[c] = x
-        return done
+        return done, cut
 
     def initialise(self):
         super().initialise()
@@ -446,9 +471,10 @@ class PrefetchSampler(ChainSampler):
         nodes = self._schedule()
         if nodes:
             self._evaluate(nodes)
-        done = self._resolve()
+        widths = [k for k in self.tuner.cands if k <= len(nodes)] if self.tuner is not None else ()
+        done, cut = self._resolve(widths)
         if self.tuner is not None and nodes:
-            self.tuner.record(self.slots, time.perf_counter() - t0, sum(self.filters_run) - f0)
+            self.tuner.record(self.slots, time.perf_counter() - t0, cut)
         self.i = min(r.i for r in self.roots)
         if self.i >= self.iters:
             self._finish()

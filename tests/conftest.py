@@ -1,4 +1,5 @@
 """Shared test setup.  `-m "not gpu"` runs on CPU; `-m gpu` needs an MI355X and libepipf.so."""
+import glob
 import os
 import sys
 
@@ -57,7 +58,12 @@ def kernels_golden():
 
 @pytest.fixture(scope="session")
 def pmcmc_golden():
-    return load_golden("pmcmc_golden.npz")
+    """The toy-shape traces (pmcmc_golden.npz) and the BASELINE-shape ones, one file per case
+    (pmcmc_<case>_golden.npz: cfg1_full, test_pmcmc_p; make_golden.py PMCMC_BASELINE_CASES)."""
+    out = dict(load_golden("pmcmc_golden.npz"))
+    for path in sorted(glob.glob(os.path.join(GOLDEN, "pmcmc_*_golden.npz"))):
+        out.update(load_golden(os.path.basename(path)))
+    return out
 
 
 @pytest.fixture(scope="session")

@@ -254,11 +254,13 @@ def test_dropin_particle_filter_signature(filter_golden):
         (None, None, None)
 
 
-@pytest.mark.parametrize("prefetch", [0, 32])
-@pytest.mark.parametrize("name", ["sir_small", "sir_p", "sub", "sir_adaptive"])
+@pytest.mark.parametrize("prefetch", [0, 32, "auto"])
+@pytest.mark.parametrize("name", ["sir_small", "sir_p", "sub", "sir_adaptive", "cfg1_full", "test_pmcmc_p"])
 def test_pmcmc_matches_reference_golden(pmcmc_golden, name, prefetch):
     """particle_mcmc under np.random.seed(s) + seed_stream(key): identical accept/reject trace, thetas,
-    sampled trajectories; likelihoods within 1e-9 relative."""
+    sampled trajectories; likelihoods within 1e-9 relative.  cfg1_full is BASELINE config 1 itself (N=100, pop 200,
+    T=50, 500 MH iterations) and test_pmcmc_p the reference's tests/test_pmcmc_p.py shape (N=100, pop 4820, T=15,
+    probs=None, h=5 and its Sigma), both run through the unmodified reference (tests/golden/make_golden.py)."""
     from epipf import particle_mcmc, seed_stream
     rec = pmcmc_golden["pmcmc_" + name]
     model = str(rec["model"])

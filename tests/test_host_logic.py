@@ -14,7 +14,7 @@ def oracle_engine(monkeypatch):
     monkeypatch.setattr(pm, "get_engine", fake_get_engine)
 
 
-@pytest.mark.parametrize("name", ["sir_small", "sir_p", "sub"])
+@pytest.mark.parametrize("name", ["sir_small", "sir_p", "sub", "cfg1_full", "test_pmcmc_p"])
 def test_mh_loop_reproduces_reference_trace(oracle_engine, pmcmc_golden, name):
     rec = pmcmc_golden["pmcmc_" + name]
     model = str(rec["model"])

@@ -170,3 +170,50 @@ def test_slot_tuner_picks_the_best_measured_rate():
         t.record(k, cost[k] * (50.0 if k not in first else 1.0))     # a slow first round per width: not timed
         first.add(k)
     assert t.best == 4
+
+
+@pytest.mark.parametrize("chains,h", [(1, 0.01), (1, 0.1), (2, 0.03)])
+def test_round_cuts_equal_narrower_rounds(datasets_golden, chains, h):
+    """The tuner's observed yields (SlotTuner, PrefetchSampler._resolve): the filters a K-slot round commits when its
+    realised path is cut at the first node of schedule rank >= K' equal what a K'-slot round commits from the same
+    state (best-first scheduling: the K' most probable nodes are the same), for every K' < K."""
+    Y = datasets_golden["cfg1_binom"][:12]
+    kw = dict(iters=40, probs=0.1, n_particles=24, n_population=200.0, mu=20.0, mh_ratio="log")
+
+    def sampler(slots):
+        s = pf.PrefetchSampler(Y, "sir", [2.0, 1.0], h, **kw, rngs=[np.random.RandomState(5 + c) for c in range(chains)],
+                               keys=[pm.chain_key(5, c) for c in range(chains)], slots=slots)
+        s.initialise()
+        return s
+
+    for rounds in range(3):                      # the first rounds from the same state (earlier rounds at width 12)
+        wide = sampler(12)
+        for _ in range(rounds):
+            wide.advance()
+        f0 = sum(wide.filters_run)
+        nodes = wide._schedule()
+        wide._evaluate(nodes)
+        _, cut = wide._resolve([1, 2, 4, 8, 12])
+        assert cut[12] == sum(wide.filters_run) - f0
+        for k in (1, 2, 4, 8):
+            narrow = sampler(12)
+            for _ in range(rounds):
+                narrow.advance()
+            narrow.slots = k
+            g0 = sum(narrow.filters_run)
+            narrow.advance()
+            assert cut[k] == sum(narrow.filters_run) - g0, (rounds, k)
+
+
+def test_slot_tuner_uses_observed_yields():
+    """With observed yields fed per width, the tuner follows them rather than the tree model: the model at acceptance
+    0.5 favours 8 slots at these round times, the observed cuts saturate at 4."""
+    t = pf.SlotTuner(1, 8, prior=2)
+    cost = {1: 1.0, 2: 1.0, 4: 1.0, 8: 1.3}
+    seen = {1: 1.0, 2: 2.0, 4: 3.0, 8: 3.1}
+    first = set()
+    for _ in range(60):
+        k = t.pick([0.5])
+        t.record(k, cost[k] * (50.0 if k not in first else 1.0), {kk: v for kk, v in seen.items() if kk <= k})
+        first.add(k)
+    assert t.best == 4
