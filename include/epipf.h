@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define EPIPF_ABI_VERSION 6
+#define EPIPF_ABI_VERSION 7
 
 /* return codes */
 #define EPIPF_OK 0
@@ -175,6 +175,11 @@ int epipf_abc_trials(epipf_ctx* ctx, const double* Y, int T, const double* prior
  * evaluated on the host CPU with the same code and table: out[i] = log(x[i]) bit for bit for normal x[i] > 0.
  * For tests of that restatement; no GPU involved. */
 int epipf_glibc_log(int64_t n, const double* x, double* out);
+
+/* The lane-group filter's certified-clock log (clock_log_impl, csrc/epipf_device.hpp: glibc's table path without its
+ * close-to-1 branch), on the host CPU with the same code and table: out[i] ~ log(x[i]) within the bound its clock
+ * certificate assumes (tests/test_glibc_log.py measures it).  For tests; no GPU involved. */
+int epipf_clock_log(int64_t n, const double* x, double* out);
 
 /* Profiling levels: OFF; TIMING = HIP events around the init / step kernels (step_ms, init_ms), no effect on
  * the kernels; COUNTERS = TIMING + device counters of SSA events and lane use (a few atomics per wave). */

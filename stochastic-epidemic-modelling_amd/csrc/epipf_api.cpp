@@ -697,6 +697,14 @@ int epipf_glibc_log(int64_t n, const double* x, double* out) {
     return EPIPF_OK;
 }
 
+int epipf_clock_log(int64_t n, const double* x, double* out) {
+    if (n < 0 || (n > 0 && (!x || !out))) return fail(EPIPF_EINVAL, "NULL argument");
+    LogTab lt[kLogTabEntries];
+    glibc_log_table(lt);
+    for (int64_t i = 0; i < n; ++i) out[i] = clock_log_impl(x[i], lt);
+    return EPIPF_OK;
+}
+
 int epipf_resample(epipf_ctx* c, int n, const double* w, const double* u, int32_t* out, int64_t* fallbacks_out) {
     if (!c || !w || !u || !out) return fail(EPIPF_EINVAL, "NULL argument");
     if (n < 1) return fail(EPIPF_EINVAL, "n must be >= 1");

@@ -160,6 +160,36 @@ __host__ __device__ inline double glibc_log_impl(double x, const LogTab* __restr
 __device__ __noinline__ double glibc_log(double x, const LogTab* __restrict__ tab) { return glibc_log_impl(x, tab); }
 __device__ __forceinline__ double glibc_log_inl(double x, const LogTab* __restrict__ tab) { return glibc_log_impl(x, tab); }
 
+// -log(x) for the lane-group filter's certified clock (epipf_group.hpp, group_propagate<FASTCLK>), where the time only
+// has to lie within a certified bound of the reference's, not equal it: glibc's table path for every x (no branch
+// for x near 1, no compensated hi/lo sums), ~12 f64 operations instead of both of glibc's paths (a wave's 64 lanes
+// almost always hold an x on each side of its branch).  Error against the 64-bit-mantissa log over 1.2e8 inputs
+// x = 1 - U (U uniform, U small: x near 1, U near 1: x tiny; tests/test_glibc_log.py::test_clock_log_error_bound):
+//   |L' - L| <= kClockLogRel |L'|  where L' >= 2^-10  (largest seen 2.9 ulps: 8 allowed), and
+//   |L' - L| <= kClockLogAbs       where L' <  2^-10  (largest seen 2^-60.3: 2^-58 allowed; near x = 1 the table
+//                                                      entries' log c cancel against log1p(r))
+// The clock bound takes the relative part into kClockEps and the absolute part, times each such event's 1/sum(a), into
+// its own term (group_propagate).
+constexpr double kClockLogRel = 0x1.0p-50, kClockLogAbs = 0x1.0p-58;
+__host__ __device__ inline double clock_log_impl(double x, const LogTab* __restrict__ tab) {
+    const uint64_t ix = __builtin_bit_cast(uint64_t, x);
+    const uint64_t tmp = ix - 0x3FE6000000000000ull;                  // OFF
+    const int i = (int)((tmp >> 45) & 127);
+    const int k = (int)((int64_t)tmp >> 52);
+    const double z = __builtin_bit_cast(double, ix - (tmp & 0xFFF0000000000000ull));
+    const LogTab e = tab[i];
+    const double r = fma(z, e.invc, -1.0);                            // z/c - 1, |r| < 2^-8
+    const double w = fma((double)k, 0x1.62e42fefa39efp-1, e.logc);    // k ln2 + log c
+    const double r2 = r * r;
+    const double P = fma(fma(r, kGlibcLogA[4], kGlibcLogA[3]), r2, fma(r, kGlibcLogA[2], kGlibcLogA[1]));
+    return w + fma(r * r2, P, fma(r2, kGlibcLogA[0], r));            // log c + k ln2 + log1p(r)
+}
+
+// -log(1 - U) for the certified clock (clock_log_impl), 1 - U exact
+__device__ __forceinline__ double clock_neg_log_one_minus_u01(uint32_t lo, uint32_t hi, const LogTab* __restrict__ tab) {
+    return -clock_log_impl(one_minus_u01(lo, hi), tab);
+}
+
 // glibc's {invc, logc} table as the device keeps it (copied into each context, then into LDS by the waves that
 // run the exact loop)
 inline void glibc_log_table(LogTab* out) {

@@ -152,6 +152,29 @@ __device__ __forceinline__ uint32_t group_inclusive_scan(uint32_t v) {
     return v;
 }
 
+// The same inclusive prefix for doubles (the certified clock's event times, group_propagate<FASTCLK>): per level two DPP
+// moves of the halves and one v_add_f64 (64-bit adds take no DPP operand).  Lanes whose source lies outside the group
+// add +0.0, exact for the nonnegative times.
+template <int W>
+__device__ __forceinline__ double group_inclusive_scan_f64(double v) {
+    auto level = [&](auto KK) __attribute__((always_inline)) {
+        constexpr int k = decltype(KK)::value;
+        if constexpr (k < W) {
+            const uint64_t b = __double_as_longlong(v);
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x110 + k, 0xF, 0xF, true);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x110 + k, 0xF, 0xF, true);
+            double t = __longlong_as_double(((uint64_t)hi << 32) | lo);
+            if constexpr (W < 16) t = __builtin_amdgcn_inverse_ballot_w64(group_tail_mask(W, k)) ? t : 0.0;
+            v = v + t;
+        }
+    };
+    level(std::integral_constant<int, 1>{});
+    level(std::integral_constant<int, 2>{});
+    level(std::integral_constant<int, 4>{});
+    level(std::integral_constant<int, 8>{});
+    return v;
+}
+
 // The chunk's channel decisions as a fixed point (round 4), instead of W dependent decisions in event order.  With
 // d_e = f_e(x_e) the decision of event e on the state x_e before it (decide_lo's Tlo side: F::outcome) and
 // x_e = x_0 + sum_{k<e} delta(d_k), guesses g are iterated as g'_e = f_e(x_0 + sum_{k<e} delta(g_k)), all events at
@@ -217,15 +240,22 @@ __device__ __forceinline__ double exact_scale(const F& s, const ChainParam& cp) 
     }
 }
 
-// The certified clock of group_propagate<FASTCLK> (round 4).  The exact loop's tau divides every infection propensity
-// by the population (IEEE) and sum(a) into 1 (IEEE); here the propensities are multiplied by rN = fl(1 / N) instead
-// (a_i' = a_i (1 + e_i), |e_i| <= 3u: fl(q / N) vs fl(q fl(1/N)) for the same q), summed in the same order (positive
-// terms: the partial sums' relative difference grows by <= 2u per term, <= 3u + 2u n_ch), and sum(a')'s reciprocal is
-// still an IEEE division: tau' = tau (1 + e), |e| <= 3u + 2u n_ch + 4u <= 47u for G <= 4 (n_ch <= 20) -- kClockEps =
-// 128u.  The sums t' = fl(t' + tau') then differ from the exact loop's t by at most D_n = (kClockEps + 2.01 u n) t'_n
-// after n events of the step (each add rounds both sides), bounded with margin by (kClockEps + 4u n) 2 tmax near tmax.
-// An event with t' < tmax - D is inside the step as in the exact loop, one with t' > tmax + D outside; in between
-// (probability ~ D times the event rate, ~1e-9 per particle-step) the particle-step is redone on the exact clock.
+// The certified clock of group_propagate<FASTCLK> (rounds 4-5).  The exact loop's tau divides every infection
+// propensity by the population (IEEE) and sum(a) into 1 (IEEE), and takes glibc's log; here
+//   * the propensities are multiplied by rN = fl(1 / N) (a_i' = a_i (1 + e_i), |e_i| <= 3u: fl(q / N) vs fl(q fl(1/N))
+//     for the same q) and summed in the same order (positive terms: <= 3u + 2u n_ch relative);
+//   * sum(a')'s reciprocal is v_rcp_f64 refined by two Newton steps (<= 3u relative; approx_scale);
+//   * -log(1 - U) is clock_log_impl's (epipf_device.hpp): |L' - L| <= kClockLogRel L' (+ 1u for glibc's own rounding)
+//     where L' >= 2^-10, and kClockLogAbs absolute below;
+// so tau' = tau (1 + e) + scale' d, |e| <= (3 + 2 n_ch + 3 + 3)u + kClockLogRel <= 49u + 8u for G <= 4 (n_ch <= 20),
+// inside kClockEps = 128u, and d = kClockLogAbs for the events with L' < 2^-10 (0.1%; their scale' is summed into
+// the bound, `dabs`), else 0.  The times are summed per chunk by a prefix over the group (group_inclusive_scan_f64:
+// <= log2 W roundings inside the chunk, one for each slot offset and one for t + prefix, each at most u t') where the
+// exact loop adds them in order (one rounding per event): together < 3u per event of the chunk, so after n events of
+// the step the certified clock is within D_n = (kClockEps + 4u n) t'_n + dabs of the exact loop's, bounded with margin
+// by (kClockEps + 4u n) 2 tmax + dabs near tmax.  An event with t' < tmax - D is inside the step as in the exact loop,
+// one with t' > tmax + D outside; in between (probability ~ D times the event rate, ~1e-9 per particle-step) the
+// particle-step is redone on the exact clock.
 constexpr double kClockEps = 0x1.0p-46, kClockPerEvent = 0x1.0p-51;
 
 // sum(a')'s reciprocal (see above); `ok` false when it is not a positive finite number (then the exact clock decides)
@@ -247,7 +277,12 @@ __device__ __forceinline__ double approx_scale(const F& s, const ChainParam& cp,
         }
     }
     ok = d > 0x1.0p-1000 && d < 0x1.0p1000;
-    return 1.0 / d;
+    // 1/d: v_rcp_f64 (~2^-26 relative) and two Newton steps, <= 3u (the IEEE division's scaling steps are not needed
+    // on [2^-1000, 2^1000]; outside it `ok` sends the particle-step to the exact clock)
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(fma(-d, r, 1.0), r, r);
+    r = fma(fma(-d, r, 1.0), r, r);
+    return r;
 }
 
 template <int MODEL, int G, class F>
@@ -328,6 +363,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
     }
     const float kB = F::kBand * cp.band_slack;           // the decision band (slack 1: kBand, exact in ulo)
     const double rN = FASTCLK ? 1.0 / population_of<MODEL, G>(st) : 0.0;   // fl(1 / N), once per particle-step
+    double dabs = 0.0;                                   // FASTCLK: the clock log's absolute errors so far (bound term)
     F mine[K];                                           // mine[k]: state before event k W + gl
 #pragma unroll
     for (int k = 0; k < K; ++k) mine[k] = st;            // the particle-step's constants; the counts kept per event
@@ -347,7 +383,10 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
             r[k] = philox(base + (uint32_t)(k * W + gl), j, ptag, cp.f, key0, key1);
             const float uc = __uint_as_float(0x3F800000u | (r[k].w >> 9)) - (1.0f - kUlpF);   // uf + 2^-24
             ulo[k] = uc - kB;
-            L[k] = neg_log_one_minus_u01<true>(r[k].x, r[k].y, tab);                     // -log(1 - U), :62
+            if constexpr (FASTCLK)
+                L[k] = clock_neg_log_one_minus_u01(r[k].x, r[k].y, tab);                  // within the clock's bound
+            else
+                L[k] = neg_log_one_minus_u01<true>(r[k].x, r[k].y, tab);                 // -log(1 - U), :62
         }
         // sched_barrier(0) fences between the phases (draws | decision pass | extinction + redo | tau | clock): the
         // scheduler otherwise hoists independent work across the latency-bound passes (measured +1% at config 5,
@@ -398,14 +437,17 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         EPIPF_PHASE_MARK(tD);
         double tau[K];                                   // each event's time: the exact loop's expressions, or
         bool scale_ok = true;                            // FASTCLK's (approx_scale)
+        double small = 0.0;                              // FASTCLK: sum of scale' over this lane's events with L' < 2^-10
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             tau[k] = 0.0;
             if (k * W + gl < nk) {
                 if constexpr (FASTCLK) {
                     bool ok;
-                    tau[k] = approx_scale<MODEL, G>(mine[k], cp, rN, ok) * L[k];
+                    const double sc = approx_scale<MODEL, G>(mine[k], cp, rN, ok);
+                    tau[k] = sc * L[k];
                     scale_ok = scale_ok && ok;
+                    small += L[k] < 0x1.0p-10 ? sc : 0.0;
                 } else {
                     tau[k] = exact_scale<MODEL, G>(mine[k], cp) * L[k];
                 }
@@ -413,62 +455,80 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         }
         if constexpr (FASTCLK) {                         // group-uniform
             if ((__ballot(!scale_ok) >> gb) & ((1ull << W) - 1ull)) return -1;
+            // the clock log's absolute error on small logs (rare: ~0.1% of events), summed over the group; 4 ulps of
+            // margin for the f64 sum of the positive scale' terms
+            if (__any(small != 0.0)) {
+                const double s = group_lane_f64<W, W - 1>(group_inclusive_scan_f64<W>(small));
+                dabs = dabs + s * (kClockLogAbs * (1.0 + 0x1.0p-50));
+            }
         }
-        // t + tau in event order (the exact loop's additions); the step ends at the first t + tau > tmax.  Branch-free:
-        // the sum runs on through the chunk (events past nk add tau = 0) and `inside` counts the events before the
-        // first overshoot -- once an event overshoots, t is no longer needed (the step ends in this chunk).
         double tt = t;
         int inside = 0;
         __builtin_amdgcn_sched_barrier(0);
         EPIPF_PHASE_MARK(tE);
+        if constexpr (FASTCLK && !Days::kOn) {
+            // the certified clock: every event's time at once, t + its prefix over the group (no LDS, no pass in
+            // event order); the first event not surely inside ends the step there, or, within the bound, the
+            // particle-step goes to the exact clock
+            double ttk[K];
+            double off = 0.0;
 #pragma unroll
-        for (int k = 0; k < K; ++k) xch[k * 64 + lane] = tau[k];
-        lds_sync<true>();                                // this wave's stores before its loads
-        const double* xg = xch + gb;                     // tau of event e: xg[(e / W) * 64 + e % W]
-        if constexpr (Days::kOn) {
-            bool alive = true;
-            auto clock = [&](auto I) __attribute__((always_inline)) -> bool {
-                constexpr int e = decltype(I)::value;
-                tt = tt + xg[(e / W) * 64 + e % W];
-                alive = alive && !(tt > tmax);               // :65-66
-                inside += alive ? 1 : 0;
-                if (alive && e < nk) days->passed(tt, gl == e % W, mine[e / W], x0);   // days before event e (rare)
-                return true;
-            };
-            StaticFor<0, E>::run(clock);
-        } else {
-            // The sums t + tau are nondecreasing (tau >= 0; finite on this path: f32-eligible rates and counts), so
-            // every prefix is at most the chunk's total: when the total stays inside the step, so does every event,
-            // and only a chunk that overshoots (the step's last) counts the events before its first t + tau > tmax,
-            // adding again in the same order.
-            auto clock = [&](auto I) __attribute__((always_inline)) -> bool {
-                constexpr int e = decltype(I)::value;
-                tt = tt + xg[(e / W) * 64 + e % W];
-                return true;
-            };
-            StaticFor<0, E>::run(clock);
-            if constexpr (FASTCLK) {
-                // D: the bound on |t' - t| for the events up to this chunk's end (kClockEps, above; clock_slack >= 1
-                // widens it in tests so that particle-steps take the exact clock on purpose)
-                const double D = (kClockEps + kClockPerEvent * (double)(nev + E)) * (2.0 * tmax) * (double)cp.clock_slack;
-                if (tt < tmax - D) {
-                    inside = E;
-                } else {                                 // the step's last chunk: the first event not surely inside
-                    double t2 = t;
-                    bool alive = true, unsure = false;
-                    auto recount = [&](auto I) __attribute__((always_inline)) -> bool {
-                        constexpr int e = decltype(I)::value;
-                        t2 = t2 + xg[(e / W) * 64 + e % W];
-                        const bool in = t2 < tmax - D;
-                        unsure = unsure || (alive && !in && !(t2 > tmax + D));
-                        alive = alive && in;
-                        inside += alive ? 1 : 0;
-                        return true;
-                    };
-                    StaticFor<0, E>::run(recount);
-                    if (unsure) return -1;               // group-uniform: the same sums in every lane
-                }
+            for (int k = 0; k < K; ++k) {
+                const double P = group_inclusive_scan_f64<W>(tau[k]);
+                const double Pk = k == 0 ? P : off + P;
+                ttk[k] = t + Pk;
+                if (k + 1 < K) off = group_lane_f64<W, W - 1>(Pk);
+            }
+            const double D = (kClockEps + kClockPerEvent * (double)(nev + E)) * (2.0 * tmax) * (double)cp.clock_slack +
+                             dabs;
+            int first = E;
+#pragma unroll
+            for (int k = K - 1; k >= 0; --k) {
+                const uint32_t bits = (uint32_t)(__ballot(!(ttk[k] < tmax - D)) >> gb) & ((1u << W) - 1u);
+                if (bits) first = min(first, k * W + (int)__builtin_ctz(bits));
+            }
+            if (first == E) {
+                inside = E;
+                tt = group_lane_f64<W, W - 1>(ttk[K - 1]);
             } else {
+                bool unsure = false;
+#pragma unroll
+                for (int k = 0; k < K; ++k) unsure = unsure || (k * W + gl == first && !(ttk[k] > tmax + D));
+                if ((__ballot(unsure) >> gb) & ((1ull << W) - 1ull)) return -1;   // group-uniform
+                inside = first;
+            }
+        } else {
+            // the exact loop's clock: t + tau in event order (the exact loop's additions), the group's tau read from LDS
+            // (one store per lane and shared loads instead of two DPP / swizzle moves per event, which took the place
+            // of VALU issue slots); the step ends at the first t + tau > tmax.  Branch-free: the sum runs on through the
+            // chunk (events past nk add tau = 0) and `inside` counts the events before the first overshoot -- once an
+            // event overshoots, t is no longer needed (the step ends in this chunk).
+#pragma unroll
+            for (int k = 0; k < K; ++k) xch[k * 64 + lane] = tau[k];
+            lds_sync<true>();                            // this wave's stores before its loads
+            const double* xg = xch + gb;                 // tau of event e: xg[(e / W) * 64 + e % W]
+            if constexpr (Days::kOn) {
+                bool alive = true;
+                auto clock = [&](auto I) __attribute__((always_inline)) -> bool {
+                    constexpr int e = decltype(I)::value;
+                    tt = tt + xg[(e / W) * 64 + e % W];
+                    alive = alive && !(tt > tmax);       // :65-66
+                    inside += alive ? 1 : 0;
+                    if (alive && e < nk) days->passed(tt, gl == e % W, mine[e / W], x0);   // days before event e (rare)
+                    return true;
+                };
+                StaticFor<0, E>::run(clock);
+            } else {
+                // The sums t + tau are nondecreasing (tau >= 0; finite on this path: f32-eligible rates and counts), so
+                // every prefix is at most the chunk's total: when the total stays inside the step, so does every
+                // event, and only a chunk that overshoots (the step's last) counts the events before its first
+                // t + tau > tmax, adding again in the same order.
+                auto clock = [&](auto I) __attribute__((always_inline)) -> bool {
+                    constexpr int e = decltype(I)::value;
+                    tt = tt + xg[(e / W) * 64 + e % W];
+                    return true;
+                };
+                StaticFor<0, E>::run(clock);
                 if (!(tt > tmax)) {
                     inside = E;
                 } else {
@@ -477,7 +537,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
                     auto recount = [&](auto I) __attribute__((always_inline)) -> bool {
                         constexpr int e = decltype(I)::value;
                         t2 = t2 + xg[(e / W) * 64 + e % W];
-                        alive = alive && !(t2 > tmax);       // :65-66
+                        alive = alive && !(t2 > tmax);   // :65-66
                         inside += alive ? 1 : 0;
                         return true;
                     };

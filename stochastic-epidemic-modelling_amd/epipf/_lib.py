@@ -16,14 +16,14 @@ SIR, SEIR, SIR_SUBGROUPS, SIR_SUBGROUPS2 = 0, 1, 2, 3
 OBS_BINOMIAL, OBS_NORMAL = 0, 1
 RESAMPLE_MULTINOMIAL, RESAMPLE_SYSTEMATIC = 0, 1
 PROFILE_OFF, PROFILE_TIMING, PROFILE_COUNTERS = 0, 1, 2
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 EXPORTS = (
     "epipf_create", "epipf_destroy", "epipf_set_observations", "epipf_set_population", "epipf_run",
     "epipf_copy_history", "epipf_path_sample", "epipf_simulate", "epipf_resample", "epipf_set_profiling",
     "epipf_get_stats", "epipf_reset_stats", "epipf_set_streams", "epipf_set_lanes", "epipf_last_error", "epipf_abi_version", "epipf_device_count",
     "epipf_build_id",
-    "epipf_abc", "epipf_abc_trials", "epipf_glibc_log", "epipf_simulate_path",
+    "epipf_abc", "epipf_abc_trials", "epipf_glibc_log", "epipf_clock_log", "epipf_simulate_path",
 )
 
 
@@ -95,6 +95,7 @@ def load():
         "epipf_abc": ([P, P, i32, i32, f64, P, u64, u32, ctypes.c_int64, i32, P, P, P, P], i32),
         "epipf_abc_trials": ([P, P, i32, P, u64, u32, u32, i32, P, P, P, P], i32),
         "epipf_glibc_log": ([ctypes.c_int64, P, P], i32),
+        "epipf_clock_log": ([ctypes.c_int64, P, P], i32),
         "epipf_simulate_path": ([P, i32, P, P, i32, f64, u64, u32, u32, i32, P, P, P, P], i32),
     }
     for name, (args, res) in sig.items():
