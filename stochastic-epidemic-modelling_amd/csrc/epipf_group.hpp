@@ -689,9 +689,7 @@ __global__ __launch_bounds__(PB * W) void pf_step_group_kernel(StepArgs a, int p
 #pragma unroll
         for (int c = 0; c < C; ++c) x0[c] = (double)rows[pl * C + c];
         const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
-        // the certified clock pays where tau has many divisions (subgroup models: 2G + G^2 propensities; config 5 +3-6%),
-        // and costs 4-6% on SIR / SEIR's two or three (profiles/r4o_block_clock_ab.txt): the exact clock there
-        constexpr bool kFastClock = MODEL != kSIR && MODEL != kSEIR;
+        constexpr bool kFastClock = true;
         nev = group_propagate<MODEL, G, W, K, NoDays, kFastClock>(x0, x, cp, (uint32_t)jg, ptag, 1.0, tab,
                                                                   xch + wave * 64 * K, (NoDays*)nullptr, ph);
         if (kFastClock && nev < 0)                       // a clock decision within the certified clock's bound (rare)
