@@ -467,8 +467,15 @@ def config_runs(ctx, args):
             else:
                 entry["fixed_theta"] = run_summary(run)
         if chains == 1 and ctx.rank == 0 and ctx.world == 1:
+            # at the config's proposal (config 5: h = 1, acceptance often 0 over a segment: each round then commits about
+            # as many iterations as it has slots) and at the near-fixed theta (acceptance ~0.6: the speculation tree's
+            # other extreme); the acceptance is reported beside each
             entry["prefetch_auto"] = prefetch_chain(args, run["Y"], run["meta"], run["N"], run["T"], ctx.local, "auto",
                                                     160, h=entry["h"], sigma=run["meta"]["sigma"])
+            fh, fs, _ = proposal(run["meta"], "fixed_theta")
+            if fh != entry["h"]:
+                entry["prefetch_auto_fixed_theta"] = prefetch_chain(args, run["Y"], run["meta"], run["N"], run["T"],
+                                                                    ctx.local, "auto", 160, h=fh, sigma=fs)
         if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline and args.configs_cpu_seconds > 0 \
                 and name not in cpu_done:
             # the same CPU baseline as the headline's, per config, on a capped particle count

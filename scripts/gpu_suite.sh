@@ -14,7 +14,7 @@ step() {  # step <name> <timeout> <cmd...>
     if [ $rc -ne 0 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
 }
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
+step pytest_gpu ${PYTEST_T:-900} python -u -m pytest tests -m gpu -x -q -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
 step bench 400 python bench.py --steps ${STEPS:-10} --warmup 2
 if [ -n "${ABC:-}" ]; then step abc_bench 300 python scripts/abc_bench.py --runs 3 --cpu-seconds 2; fi
 echo "== done"

@@ -176,7 +176,9 @@ class SlotTuner:
     (not timed: a first launch shape pays one-off costs) and then `tries` times, T(K) the median of its last five rounds
     (a round lasts as long as its slowest filter, and the filters' costs vary with their theta: at config 5's h = 1 a
     fastest-of-three estimate picked 4 slots in one run and 1 in another, profiles/r4y_prefetch_cfg5.txt); the best and
-    its neighbours re-measured every `refresh` rounds.
+    its neighbours re-measured every `refresh` rounds, an interval that doubles (up to `refresh_max`) each time the
+    re-measurement leaves the best width where it was and starts again at `refresh` when it moves it (a refresh round
+    at twice the width costs about two rounds: at a fixed interval of 24 it cost config 2 ~5-9%, BENCH_r05).
     E(K) is OBSERVED, not modelled: the scheduler is best-first, so the K' < K most probable nodes of a K-slot round are
     exactly what a K'-slot round would have run from the same root, and a round at width K therefore also tells what
     every narrower width would have committed (PrefetchSampler._resolve: the realised path cut at its first node of
@@ -185,7 +187,7 @@ class SlotTuner:
     few (weight `prior` rounds) -- on its own it overstated wide rounds (config 2, acceptance 0.08: E(32) / E(16) = 1.28
     modelled, 1.07 observed, so 32 slots were picked and ran 10% slower than 16, BENCH_r04)."""
 
-    def __init__(self, lo, hi, tries=3, refresh=24, reeval=8, prior=2, window=64):
+    def __init__(self, lo, hi, tries=3, refresh=24, reeval=8, prior=2, window=64, refresh_max=384):
         self.cands = sorted({lo} | {k for k in (1, 2, 4, 8, 16, 32, 64, 128) if lo <= k <= hi} | {hi})
         self.samples = {k: [] for k in self.cands}          # K -> the last round times (s)
         self.count = {k: 0 for k in self.cands}              # rounds run at K (the first is a warm-up)
@@ -195,6 +197,9 @@ class SlotTuner:
         self.rounds = 0
         self.best = None
         self._next_eval = 0
+        self.refresh0, self.refresh_max = refresh, refresh_max
+        self._next_refresh = None                            # round of the next neighbour re-measurement
+        self._refreshes = 0
 
     def time(self, k):
         return float(np.median(self.samples[k][-5:]))
@@ -207,11 +212,20 @@ class SlotTuner:
         # heap expansion for every width; per round it cost ~5% of a 2-slot config-5 round in Python)
         if self.best is None or self.rounds >= self._next_eval:
             E = expected_iterations_upto(self.cands[-1], alphas, deltas)
-            self.best = max(self.cands, key=lambda k: self.yield_of(k, E[k - 1]) / self.time(k))
+            best = max(self.cands, key=lambda k: self.yield_of(k, E[k - 1]) / self.time(k))
+            if self.best is not None and best != self.best:  # the width moved: re-measure its neighbours often again
+                self.refresh = self.refresh0
+            self.best = best
             self._next_eval = self.rounds + self.reeval
-        if self.rounds % self.refresh == 0:                 # keep the neighbours' times current, alternately
+        if self._next_refresh is None:
+            self._next_refresh = self.rounds + self.refresh
+        if self.rounds >= self._next_refresh:               # keep the neighbours' times current, alternately
+            self._refreshes += 1
+            self._next_refresh = self.rounds + self.refresh
+            if self._refreshes % 2 == 0:                    # both neighbours seen since the last change: back off
+                self.refresh = min(self.refresh_max, 2 * self.refresh)
             i = self.cands.index(self.best)
-            j = i - 1 if (self.rounds // self.refresh) % 2 == 0 else i + 1
+            j = i - 1 if self._refreshes % 2 == 1 else i + 1
             if not 0 <= j < len(self.cands):
                 j = i + 1 if j < i else i - 1
             if 0 <= j < len(self.cands):
