@@ -66,6 +66,6 @@ for w in (1, 0):
     dt = time.perf_counter() - t0
     print(f"batched run of the {len(live)} live chains, lanes {w or 'auto'}: {dt * 1e3:.2f} ms, "
           f"{len(live) * N * T / dt:.3e} particle-steps/s")
-with open(os.path.join(REPO, "gpurun_out", f"r4v_chain_cost_cfg{cfg}.jsonl"), "w") as f:
+with open(os.path.join(REPO, "gpurun_out", f"chain_cost_cfg{cfg}.jsonl"), "w") as f:
     for r in rows:
         f.write(json.dumps(r) + "\n")

@@ -1,0 +1,42 @@
+#!/bin/bash
+# Closing measurement of a build: rocprofv3 trace + PMC passes (scripts/profile.sh) of every workload the bench line
+# reports -- the headline (config 2, 256 chains -> profiles/pmc_step_kernel.json), configs 1, 3, 4, 5 at 256 chains
+# (pmc_group_cfg1.json, pmc_step_cfg{3,4,5}.json) and config 5 at one chain per GPU (pmc_group_cfg5_c1.json) -- each
+# recording the library's build id, so the bench line's rooflines are those of the library it times; then the default
+# bench line and the ABC bench.  Each step has its own time limit; a failure ends the script.
+#   TAG=r5z bash scripts/close.sh            (WHAT="c2 c1 c3 c4 c5 c5x1 bench abc" selects steps)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+T=${TAG:-close}
+WHAT=${WHAT:-c2 c1 c3 c4 c5 c5x1 bench abc}
+mkdir -p gpurun_out/$T
+has() { [[ " $WHAT " == *" $1 "* ]]; }
+prof() {  # prof <tag> <json name> <env...>
+    local tag=$1 name=$2; shift 2
+    env "$@" PMC_NAME=$name TAG=${T}_$tag bash scripts/profile.sh || exit $?
+    cp gpurun_out/prof_${T}_$tag/$name gpurun_out/$T/
+}
+has c2 && prof c2 pmc_step_kernel.json PMC_CONFIG=2 PMC_CHAINS=256
+has c1 && prof c1 pmc_group_cfg1.json PMC_CONFIG=1 PMC_CHAINS=256 PMC_LANES=16 PMC_KERNEL=pf_step_group_kernel \
+  BENCH_ARGS="--config 1" STEPS=20
+for cfg in 3 4 5; do
+  has c$cfg && prof c${cfg}x256 pmc_step_cfg$cfg.json PMC_CONFIG=$cfg PMC_CHAINS=256 BENCH_ARGS="--config $cfg"
+done
+has c5x1 && prof c5x1 pmc_group_cfg5_c1.json PMC_CONFIG=5 PMC_CHAINS=1 PMC_LANES=16 PMC_KERNEL=pf_step_group_kernel \
+  BENCH_ARGS="--config 5 --chains 1" STEPS=20
+if has bench; then
+  echo "== bench ($(date +%T))"
+  cp gpurun_out/$T/pmc_*.json profiles/ 2>/dev/null
+  timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/$T/bench.log 2>&1 || { tail -5 gpurun_out/$T/bench.log; exit 1; }
+  tail -1 gpurun_out/$T/bench.log | python3 -c "
+import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']
+print('headline', f\"{d['value']:.4e}\", 'frac', r['frac'], 'single', f\"{d['single_chain_value']:.3e}\", 'pf16', f\"{d['single_chain_prefetch']['value']:.3e}\", 'pfauto', f\"{d['single_chain_prefetch_auto']['value']:.3e}\")
+for k, e in d['configs'].items(): print(k, f\"{e['value']:.4e}\", 'frac', e['roofline']['frac'], 'lanes', e['lanes_per_particle'], 'fixed', f\"{e.get('fixed_theta', {}).get('value', 0):.3e}\", 'pf', (e.get('prefetch_auto') or {}).get('value'))"
+fi
+if has abc; then
+  echo "== abc bench ($(date +%T))"
+  timeout -k 10 300 python scripts/abc_bench.py --runs 10 --cpu-seconds 10 > gpurun_out/$T/abc_bench.log 2>&1 || { tail -5 gpurun_out/$T/abc_bench.log; exit 1; }
+  tail -1 gpurun_out/$T/abc_bench.log | cut -c1-300
+fi
+echo "== done"

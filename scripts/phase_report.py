@@ -1,7 +1,7 @@
 """Summarise the per-wave phase cycles printed by the phase-timing build of the lane-group step kernel (make phase:
 lib/libepipf_phase.so, s_memtime at the phase fences of group_propagate; diagnostic only).
 
-    python scripts/r3d_phase_report.py log..."""
+    python scripts/phase_report.py log..."""
 import collections
 import re
 import sys

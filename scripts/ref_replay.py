@@ -5,9 +5,9 @@ bench's keys, thetas around its start; launches of --slice chains), with the dev
 on the host -- scipy.stats.binom.pmf / norm.pdf weights of the device's own states, numpy legacy choice on the keyed
 uniforms (tests/reference_replay.py) -- and counts ancestors that differ.  Also reports the device's
 reference-ambiguity count (draws whose uniform lies within scipy's error envelope of a CDF boundary) and its
-uncertified draws for the same launch.  Writes profiles/r3_ref_replay_cfg<config>.json.
+uncertified draws for the same launch.  Writes gpurun_out/ref_replay_cfg<config>.json.
 
-    python scripts/r3_ref_replay.py [--config 2] [--chains 256] [--workers 12]"""
+    python scripts/ref_replay.py [--config 2] [--chains 256] [--workers 12]"""
 import argparse
 import json
 import os
@@ -86,7 +86,7 @@ def main():
                      "uniforms (pmcmc.py:185-190), tests/reference_replay.py"}
     print(json.dumps(out), flush=True)
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(REPO, "gpurun_out", f"r3_ref_replay_cfg{args.config}.json"), "w") as fh:
+    with open(os.path.join(REPO, "gpurun_out", f"ref_replay_cfg{args.config}.json"), "w") as fh:
         json.dump(out, fh, indent=1)
 
 

@@ -504,9 +504,12 @@ struct FastSsa<kSIR, 1> {                                              // gilles
     // decide_lo's Tlo side, as an event count in a byte field (byte 0 infections, byte 1 recoveries), and a state
     // rebuilt from the chunk start b and the counts n of the events before it (small integers: exact in f32)
     static constexpr bool kFixedPoint = true;
-    __device__ __forceinline__ uint32_t outcome(float ulo) const {
+    // cc / tot (optional): the cumulative rates and total it decided on, kept for the certificate (event_certified_on)
+    __device__ __forceinline__ uint32_t outcome(float ulo, float* cc = nullptr, float* tot = nullptr) const {
         float c[1];
-        const float Tlo = ulo * cum(c);
+        const float total = cum(c);
+        const float Tlo = ulo * total;
+        if (cc) { cc[0] = c[0]; *tot = total; }
         return c[0] < Tlo ? 0x100u : 0x1u;
     }
     __device__ __forceinline__ void advance(const FastSsa& b, uint32_t n) {
@@ -566,9 +569,11 @@ struct FastSsa<kSEIR, 1> {                                             // gilles
     }
     // fixed-point pass (see FastSsa<kSIR>): byte 0 S->E, byte 1 E->I, byte 2 I->R
     static constexpr bool kFixedPoint = true;
-    __device__ __forceinline__ uint32_t outcome(float ulo) const {
+    __device__ __forceinline__ uint32_t outcome(float ulo, float* cc = nullptr, float* tot = nullptr) const {
         float c[2];
-        const float Tlo = ulo * cum(c);
+        const float total = cum(c);
+        const float Tlo = ulo * total;
+        if (cc) { cc[0] = c[0]; cc[1] = c[1]; *tot = total; }
         return c[1] < Tlo ? 0x10000u : c[0] < Tlo ? 0x100u : 0x1u;
     }
     __device__ __forceinline__ void advance(const FastSsa& b, uint32_t n) {
@@ -864,9 +869,15 @@ struct FastSubgroupsPacked {                                           // gilles
     static constexpr uint32_t code(int ch) {             // the event count of channel ch, in its field
         return 1u << (8 * (ch % (G + 1) < G ? ch % (G + 1) : G + ch / (G + 1)));
     }
-    __device__ __forceinline__ uint32_t outcome(float ulo) const {
+    __device__ __forceinline__ uint32_t outcome(float ulo, float* cc = nullptr, float* tot = nullptr) const {
         float c[NCH - 1];
-        const float Tlo = ulo * cum(c);
+        const float total = cum(c);
+        const float Tlo = ulo * total;
+        if (cc) {
+#pragma unroll
+            for (int i = 0; i < NCH - 1; ++i) cc[i] = c[i];
+            *tot = total;
+        }
         uint32_t d = code(0);                            // channel = #{i : c_i < Tlo} (the c_i are nondecreasing)
 #pragma unroll
         for (int i = 0; i < NCH - 1; ++i) d = c[i] < Tlo ? code(i + 1) : d;

@@ -35,7 +35,15 @@
 
 #include "epipf_internal.hpp"
 
+
 namespace epipf {
+
+// Minimum waves per SIMD asked of the lane-group kernel's register allocation: 4 for the subgroup models (139 VGPRs,
+// 3 waves per SIMD, without it: two to four chains of 10^4 particles need 4.9-9.8 waves per SIMD; with the bound 128 VGPRs
+// and a few spills, +7% / +14% at two / four chains of config 5, unchanged at one), none for SIR / SEIR (-5-7% at four
+// chains with it; profiles/r5i_group_waves_ab.txt).
+template <int MODEL>
+constexpr int group_min_waves() { return MODEL >= kSubgroups ? 4 : 1; }
 
 // Value of lane I of this lane's group of W consecutive lanes: DPP moves (groups of W <= 16 lie inside one DPP row),
 // a swizzle for W = 8.
@@ -114,16 +122,23 @@ __device__ __forceinline__ void decide_sequential(F& st, F* mine, const float* u
     StaticFor<0, W * K>::run(decide);
 }
 
+// the certificate on cumulative rates c and total already evaluated on the state (the fixed-point pass keeps its last
+// evaluation's: the same arithmetic on the same values as a recomputation)
+template <int NCH>
+__device__ __forceinline__ bool event_certified_on(const float* c, float total, float ulo, float kB) {
+    const float Tlo = ulo * total, Thi = fmaf(2.0f * kB, total, Tlo);
+    bool sure = true;
+#pragma unroll
+    for (int i = 0; i < NCH - 1; ++i) sure = sure && ((c[i] < Tlo) == (c[i] < Thi));
+    return sure;
+}
+
 template <typename F>
 __device__ __forceinline__ bool event_certified(const F& s, float ulo, float kB) {
     constexpr int NCH = F::NCH;
     float c[NCH - 1];
     const float total = s.cum(c);
-    const float Tlo = ulo * total, Thi = fmaf(2.0f * kB, total, Tlo);
-    bool sure = true;
-#pragma unroll
-    for (int i = 0; i < NCH - 1; ++i) sure = sure && ((c[i] < Tlo) == (c[i] < Thi));
-    return sure || !s.active();
+    return event_certified_on<NCH>(c, total, ulo, kB) || !s.active();
 }
 
 // Inclusive prefix sum over this lane's group of W consecutive lanes (Hillis-Steele on DPP row shifts; a group of
@@ -186,9 +201,11 @@ __device__ __forceinline__ double group_inclusive_scan_f64(double v) {
 // slowest group needs 2.3 evaluations on average -- against 8 dependent decisions of the sequential pass.
 // With K events per lane (event k W + gl in slot k) the K slots' counts are scanned side by side and slot k's prefix is
 // offset by the totals of the slots before it.
-// On return: mine[k] = the state before event k W + gl, st = the state after the chunk (every lane of the group).
+// On return: mine[k] = the state before event k W + gl, st = the state after the chunk (every lane of the group), and
+// cc[k] / tot[k] the cumulative rates and total of mine[k] (the last evaluation's, for the certificate).
 template <int W, int K, class F>
-__device__ __forceinline__ void decide_fixed_point(F& st, F* mine, const float* ulo) {
+__device__ __forceinline__ void decide_fixed_point(F& st, F* mine, const float* ulo, float (*cc)[F::NCH - 1],
+                                                   float* tot) {
     uint32_t d[K], ex[K], total = 0;
 #pragma unroll
     for (int k = 0; k < K; ++k) d[k] = st.outcome(ulo[k]);
@@ -207,7 +224,7 @@ __device__ __forceinline__ void decide_fixed_point(F& st, F* mine, const float* 
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             mine[k].advance(st, ex[k]);
-            const uint32_t d2 = mine[k].outcome(ulo[k]);
+            const uint32_t d2 = mine[k].outcome(ulo[k], cc[k], &tot[k]);
             changed = changed || d2 != d[k];
             d[k] = d2;
         }
@@ -241,40 +258,50 @@ __device__ __forceinline__ double exact_scale(const F& s, const ChainParam& cp) 
 }
 
 // The certified clock of group_propagate<FASTCLK> (rounds 4-5).  The exact loop's tau divides every infection
-// propensity by the population (IEEE) and sum(a) into 1 (IEEE), and takes glibc's log; here
-//   * the propensities are multiplied by rN = fl(1 / N) (a_i' = a_i (1 + e_i), |e_i| <= 3u: fl(q / N) vs fl(q fl(1/N))
-//     for the same q) and summed in the same order (positive terms: <= 3u + 2u n_ch relative);
-//   * sum(a')'s reciprocal is v_rcp_f64 refined by two Newton steps (<= 3u relative; approx_scale);
+// propensity by the population (IEEE), sums the propensities in order, divides the sum into 1 (IEEE) and takes glibc's
+// log: its sum(a) is within (3 + n_ch)u of the real sum (three roundings per propensity, n_ch - 1 additions of positive
+// terms).  Here (approx_scale)
+//   * sum(a') is evaluated factored, with rN = fl(1 / N) in place of the divisions: every term positive, at most
+//     2G + 2 roundings on any path, so within (2G + 2)u of the real sum;
+//   * its reciprocal is v_rcp_f64 refined by two Newton steps (<= 3u relative; the IEEE quotient: 0.5u);
 //   * -log(1 - U) is clock_log_impl's (epipf_device.hpp): |L' - L| <= kClockLogRel L' (+ 1u for glibc's own rounding)
 //     where L' >= 2^-10, and kClockLogAbs absolute below;
-// so tau' = tau (1 + e) + scale' d, |e| <= (3 + 2 n_ch + 3 + 3)u + kClockLogRel <= 49u + 8u for G <= 4 (n_ch <= 20),
-// inside kClockEps = 128u, and d = kClockLogAbs for the events with L' < 2^-10 (0.1%; their scale' is summed into
-// the bound, `dabs`), else 0.  The times are summed per chunk by a prefix over the group (group_inclusive_scan_f64:
-// <= log2 W roundings inside the chunk, one for each slot offset and one for t + prefix, each at most u t') where the
-// exact loop adds them in order (one rounding per event): together < 3u per event of the chunk, so after n events of
-// the step the certified clock is within D_n = (kClockEps + 4u n) t'_n + dabs of the exact loop's, bounded with margin
-// by (kClockEps + 4u n) 2 tmax + dabs near tmax.  An event with t' < tmax - D is inside the step as in the exact loop,
-// one with t' > tmax + D outside; in between (probability ~ D times the event rate, ~1e-9 per particle-step) the
-// particle-step is redone on the exact clock.
+// so tau' = tau (1 + e) + scale' d with |e| <= (3 + n_ch + 2G + 2 + 3.5 + 1)u + kClockLogRel + 1u <= 34u + 8u + 1u for
+// G <= 4 (n_ch <= 20), inside kClockEps = 128u, and d = kClockLogAbs for the events with L' < 2^-10 (0.1%; their scale'
+// is summed into the bound, `dabs`), else 0.  The times are summed per chunk by a prefix over the group
+// (group_inclusive_scan_f64: <= log2 W roundings inside the chunk, one for each slot offset and one for t + prefix,
+// each at most u t') where the exact loop adds them in order (one rounding per event): together < 3u per event of the
+// chunk, so after n events of the step the certified clock is within D_n = (kClockEps + 4u n) t'_n + dabs of the exact
+// loop's, bounded with margin by (kClockEps + 4u n) 2 tmax + dabs near tmax.  An event with t' < tmax - D is inside the
+// step as in the exact loop, one with t' > tmax + D outside; in between (probability ~ D times the event rate, ~1e-9
+// per particle-step) the particle-step is redone on the exact clock.
 constexpr double kClockEps = 0x1.0p-46, kClockPerEvent = 0x1.0p-51;
 
 // sum(a')'s reciprocal (see above); `ok` false when it is not a positive finite number (then the exact clock decides)
 template <int MODEL, int G, class F>
 __device__ __forceinline__ double approx_scale(const F& s, const ChainParam& cp, double rN, bool& ok) {
+    // sum(a') factored (every term positive, each operation one rounding: <= 8u relative for G <= 4, in the budget above)
+    //   SIR  I (beta S rN + gamma);  SEIR  I (beta S rN + gamma) + alpha E;
+    //   subgroups  rN sum_g I_g sum_g2 beta[g][g2] S_g2 + gamma sum_g I_g
     double d;
     if constexpr (MODEL == kSIR) {
-        d = ((cp.theta[0] * (double)s.S) * (double)s.I) * rN + cp.theta[1] * (double)s.I;
+        d = (double)s.I * fma(cp.theta[0] * (double)s.S, rN, cp.theta[1]);
     } else if constexpr (MODEL == kSEIR) {
-        d = (((cp.theta[0] * (double)s.S) * (double)s.I) * rN + cp.theta[1] * (double)s.E) + cp.theta[2] * (double)s.I;
+        d = fma((double)s.I, fma(cp.theta[0] * (double)s.S, rN, cp.theta[2]), cp.theta[1] * (double)s.E);
     } else {
-        const double gamma = cp.theta[G * G];
-        d = 0.0;
+        double Sd[G], inf = 0.0, sI = 0.0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) Sd[g] = (double)s.S(g);
 #pragma unroll
         for (int g = 0; g < G; ++g) {
+            double row = cp.theta[g * G] * Sd[0];
 #pragma unroll
-            for (int g2 = 0; g2 < G; ++g2) d = d + ((cp.theta[g * G + g2] * (double)s.S(g2)) * (double)s.I(g)) * rN;
-            d = d + gamma * (double)s.I(g);
+            for (int g2 = 1; g2 < G; ++g2) row = fma(cp.theta[g * G + g2], Sd[g2], row);
+            const double Ig = (double)s.I(g);
+            inf = g == 0 ? row * Ig : fma(row, Ig, inf);
+            sI = g == 0 ? Ig : sI + Ig;
         }
+        d = fma(inf, rN, cp.theta[G * G] * sI);
     }
     ok = d > 0x1.0p-1000 && d < 0x1.0p1000;
     // 1/d: v_rcp_f64 (~2^-26 relative) and two Newton steps, <= 3u (the IEEE division's scaling steps are not needed
@@ -394,18 +421,24 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         __builtin_amdgcn_sched_barrier(0);
         EPIPF_PHASE_MARK(tB);
         const F st0 = st;
+        bool uncertified = false;                        // this lane's events, on the states before them
         if constexpr (F::kFixedPoint) {
             if (!(cp.flags & kChainSeqDecide)) {
-                decide_fixed_point<W, K>(st, mine, ulo);
+                float cc[K][F::NCH - 1], tot[K];
+                decide_fixed_point<W, K>(st, mine, ulo, cc, tot);
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    uncertified = uncertified || !(event_certified_on<F::NCH>(cc[k], tot[k], ulo[k], kB) || !mine[k].active());
             } else {
                 decide_sequential<W, K>(st, mine, ulo, gl);
+#pragma unroll
+                for (int k = 0; k < K; ++k) uncertified = uncertified || !event_certified(mine[k], ulo[k], kB);
             }
         } else {
             decide_sequential<W, K>(st, mine, ulo, gl);
-        }
-        bool uncertified = false;                        // this lane's events, on the states before them
 #pragma unroll
-        for (int k = 0; k < K; ++k) uncertified = uncertified || !event_certified(mine[k], ulo[k], kB);
+            for (int k = 0; k < K; ++k) uncertified = uncertified || !event_certified(mine[k], ulo[k], kB);
+        }
         __builtin_amdgcn_sched_barrier(0);
         EPIPF_PHASE_MARK(tC);
         // events up to extinction: the first e whose state before it is extinct (the last applied event emptied it)
@@ -589,7 +622,7 @@ inline size_t group_lds_bytes_impl(int B, int S, int C, int W, int K, int PB) {
 // kernel the same way).  Wave 0's first PB lanes hold the block's particles in the scan/search/gather and store/weigh
 // phases; the block is PB W / 64 waves.
 template <int MODEL, int G, int OBS, int W, int K, int PB>
-__global__ __launch_bounds__(PB * W) void pf_step_group_kernel(StepArgs a, int p) {
+__global__ __launch_bounds__(PB * W, group_min_waves<MODEL>()) void pf_step_group_kernel(StepArgs a, int p) {
     using Sh = Shape<MODEL, G>;
     constexpr int C = Sh::C;
     constexpr int PPW = 64 / W;                          // particles per wave
