@@ -132,7 +132,9 @@ static int pick_lanes(const epipf_ctx* c, int n_chains) {
     // the W = 16 rule was measured on G = 2, whose decisions run as a fixed point (FastSubgroupsPacked::kFixedPoint,
     // G <= 2); G = 3, 4 keep the sequential pass (W dependent decisions per chunk) and round 3's W = 8
     if (c->G > 2) return blocks <= lb / 2 ? 8 : blocks <= lb ? 4 : 1;
-    return blocks <= lb / 2 ? 16 : blocks <= lb ? 4 : 1;
+    // round 5 (certified group clock): W = 16 leads up to six chains of 10^4 (+10% over W = 4 at six), W = 4 at eight
+    // (profiles/r5l_lanes_pick_sweep.jsonl)
+    return blocks <= lb * 3 / 4 ? 16 : blocks <= lb ? 4 : 1;
 }
 
 // Particles per block of a run's weight layout (block sums, in-block prefixes): 64, one wave of the one-lane kernel, or

@@ -337,6 +337,15 @@ __device__ __forceinline__ double population_of(const F& s) {
 // The filter records nothing.
 // Phase timing (make phase -> lib/libepipf_phase.so, EPIPF_PHASE_TIMING): s_memtime at the phase fences of the chunk
 // loop, summed per lane group; the step kernel prints each sampled wave's totals (scripts/r3d_phase_report.py).
+// Scheduling fences between the chunk's phases (EPIPF_GROUP_FENCES=0 lets the compiler move work across them)
+#ifndef EPIPF_GROUP_FENCES
+#define EPIPF_GROUP_FENCES 1
+#endif
+#if EPIPF_GROUP_FENCES
+#define EPIPF_GROUP_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define EPIPF_GROUP_FENCE() ((void)0)
+#endif
 #ifdef EPIPF_PHASE_TIMING
 #define EPIPF_PHASE_MARK(v)                                  \
     const unsigned long long v = __builtin_readcyclecounter(); \
@@ -395,7 +404,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
 #pragma unroll
     for (int k = 0; k < K; ++k) mine[k] = st;            // the particle-step's constants; the counts kept per event
     for (;;) {
-        __builtin_amdgcn_sched_barrier(0);
+        EPIPF_GROUP_FENCE();
         EPIPF_PHASE_MARK(tA);
         Block r[K];
         float ulo[K];
@@ -418,7 +427,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         // sched_barrier(0) fences between the phases (draws | decision pass | extinction + redo | tau | clock): the
         // scheduler otherwise hoists independent work across the latency-bound passes (measured +1% at config 5,
         // one chain; profiles/r3d_phase_timing.txt has the per-phase cycles)
-        __builtin_amdgcn_sched_barrier(0);
+        EPIPF_GROUP_FENCE();
         EPIPF_PHASE_MARK(tB);
         const F st0 = st;
         bool uncertified = false;                        // this lane's events, on the states before them
@@ -439,7 +448,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
 #pragma unroll
             for (int k = 0; k < K; ++k) uncertified = uncertified || !event_certified(mine[k], ulo[k], kB);
         }
-        __builtin_amdgcn_sched_barrier(0);
+        EPIPF_GROUP_FENCE();
         EPIPF_PHASE_MARK(tC);
         // events up to extinction: the first e whose state before it is extinct (the last applied event emptied it)
         int nk = E;
@@ -466,7 +475,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
             for (int k = 0; k < K; ++k)                  // the state before event nk (< E): the extinct one
                 if (k * W + gl == nk) mine[k] = st;
         }
-        __builtin_amdgcn_sched_barrier(0);
+        EPIPF_GROUP_FENCE();
         EPIPF_PHASE_MARK(tD);
         double tau[K];                                   // each event's time: the exact loop's expressions, or
         bool scale_ok = true;                            // FASTCLK's (approx_scale)
@@ -497,7 +506,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
         }
         double tt = t;
         int inside = 0;
-        __builtin_amdgcn_sched_barrier(0);
+        EPIPF_GROUP_FENCE();
         EPIPF_PHASE_MARK(tE);
         if constexpr (FASTCLK && !Days::kOn) {
             // the certified clock: every event's time at once, t + its prefix over the group (no LDS, no pass in
@@ -578,7 +587,7 @@ __device__ __forceinline__ int group_propagate(const double* x0, double* xout, c
                 }
             }
         }
-        __builtin_amdgcn_sched_barrier(0);
+        EPIPF_GROUP_FENCE();
         EPIPF_PHASE_MARK(tF);
 #ifdef EPIPF_PHASE_TIMING
         if (ph) {

@@ -209,7 +209,7 @@ def test_lane_groups_full_size_single_chain_vs_oracle(cfg, lanes):
     if mid < 2:                                          # SIR / SEIR
         auto = 16 if blocks <= 320 else 8 if blocks <= 960 else 4
     else:
-        auto = 16 if blocks <= 640 else 4
+        auto = 16 if blocks <= 960 else 4
     assert eng.stats()["last_lanes"] == (lanes or auto)
     hid, anc = eng.history(1)
     eng.close()
@@ -223,7 +223,7 @@ def test_lane_groups_full_size_single_chain_vs_oracle(cfg, lanes):
 
 def test_automatic_lane_choice():
     """SIR / SEIR: up to two chains of 10^4 particles get 16 lanes, up to 6 chains 8, up to 8 chains 4; subgroup models:
-    16 lanes up to 4 chains, then 4 up to 8; a batch that fills the chip keeps one lane per particle."""
+    16 lanes up to 6 chains, then 4 up to 8; a batch that fills the chip keeps one lane per particle."""
     from epipf.engine import Engine
     Y = np.zeros((3, 3))
     eng = Engine("sir", 1, 10000, 3, 256)
@@ -237,7 +237,7 @@ def test_automatic_lane_choice():
     eng.set_observations(np.zeros((3, 6)))
     eng.set_population([2000, 3000], [20, 30])
     th = np.array([4.0, 1.0, 1.0, 4.0, 1.0])
-    for chains, want in [(1, 16), (4, 16), (5, 4), (8, 4), (9, 1)]:
+    for chains, want in [(1, 16), (4, 16), (6, 16), (7, 4), (8, 4), (9, 1)]:
         eng.run(np.tile(th, (chains, 1)), [0.1] * chains, list(range(1, chains + 1)), [0] * chains)
         assert eng.stats()["last_lanes"] == want, (chains, eng.stats()["last_lanes"])
     eng.close()
