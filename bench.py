@@ -64,9 +64,9 @@ def parse():
                          "others' filters (epipf.pmcmc.run_pipelined); 1 = one lockstep sampler; 0 = automatic: 2 "
                          "where the MH step is host-bound (config 1: tiny filters), else 1 (DESIGN.md §6)")
     ap.add_argument("--prefetch", type=int, default=16, help="filter slots per round of the speculative single chain")
-    # ~20 rounds: a speculative round commits ~10 iterations at config 2, so 60 iterations were 6 rounds and the
-    # adaptive width's figure moved by +-20% from run to run (profiles/r4y_prefetch_cfg5.txt)
-    ap.add_argument("--prefetch-iters", type=int, default=200, help="MH iterations timed for the speculative chain")
+    # ~40 rounds: a speculative round commits ~8 iterations at config 2; 60 iterations (6 rounds) moved the adaptive
+    # width's figure by +-20% from run to run (profiles/r4y_prefetch_cfg5.txt), 200 still by ~+-7% (BENCH_r05)
+    ap.add_argument("--prefetch-iters", type=int, default=400, help="MH iterations timed for the speculative chain")
     return ap.parse_args()
 
 
@@ -403,29 +403,34 @@ def run_summary(run):
             "events_per_s": run["value"] * cst["events"] / ps if ps else None}
 
 
-def prefetch_chain(args, Y, meta, N, T, local, slots, iters, h=1e-4, sigma=None):
+def prefetch_chain(args, Y, meta, N, T, local, slots, iters, h=1e-4, sigma=None, start=20):
     """One chain with speculative MH (epipf.prefetch): filters of future iterations share one batched launch sequence;
-    only filters on the realised path count.  slots = "auto" lets the sampler size its rounds."""
+    only filters on the realised path count.  slots = "auto" lets the sampler size its rounds.  The
+    timed window starts at MH iteration `start` (or later, once the auto width has measured every candidate): a
+    round's yield depends on the accept / reject pattern of the chain segment it covers, so two widths are compared
+    on the same segment (the auto leg first, then the fixed width from the auto leg's start)."""
     import torch
     from epipf.pmcmc import chain_key
     from epipf.prefetch import PrefetchSampler
-    s2 = PrefetchSampler(Y, meta["model"], list(meta["theta"]), h, sigma=sigma, iters=iters + 200, probs=meta["probs"],
+    s2 = PrefetchSampler(Y, meta["model"], list(meta["theta"]), h, sigma=sigma, iters=start + iters + 1000,
+                         probs=meta["probs"],
                          observations=meta.get("observations", False), n_particles=N,
                          n_population=meta["n_population"], mu=meta["mu"],
                          rngs=[np.random.RandomState(args.seed)], keys=[chain_key(args.seed, 0)], device=local,
                          mh_ratio="log", slots=slots)
     s2.initialise()
-    while s2.i < 20 or not s2.tuned:                 # slots="auto": warm up until every width has been measured
+    while s2.i < start or not s2.tuned:              # slots="auto": warm up until every width has been measured
         s2.advance()
     torch.cuda.synchronize()
     i0, f0, r0, sp0, a0 = s2.i, s2.filters_run[0], s2.rounds, s2.speculative_filters, s2.acceptances[0]
+    assert i0 + iters <= s2.iters, (i0, iters, s2.iters)   # the auto width's warm-up ends within the sampler's span
     t2 = time.perf_counter()
     while s2.i < i0 + iters:
         s2.advance()
     torch.cuda.synchronize()
     dt2 = time.perf_counter() - t2
     return {"value": (s2.filters_run[0] - f0) * N * T / dt2, "slots": slots, "slots_used": s2.slots,
-            "iterations": s2.i - i0, "rounds": s2.rounds - r0,
+            "start_iteration": i0, "iterations": s2.i - i0, "rounds": s2.rounds - r0,
             "iterations_per_round": (s2.i - i0) / max(1, s2.rounds - r0),
             "filters_evaluated": s2.speculative_filters - sp0,
             "acceptance_rate": (s2.acceptances[0] - a0) / max(1, s2.filters_run[0] - f0),
@@ -568,10 +573,10 @@ def main():
         f1 = sum(s1.step() for _ in range(args.steps))
         torch.cuda.synchronize()
         single = f1 * N * T / (time.perf_counter() - t1)
-        prefetch = prefetch_chain(args, Y, meta, N, T, local, args.prefetch, args.prefetch_iters, h=run["h"],
-                                  sigma=run["sigma"])
         prefetch_auto = prefetch_chain(args, Y, meta, N, T, local, "auto", args.prefetch_iters, h=run["h"],
                                        sigma=run["sigma"])
+        prefetch = prefetch_chain(args, Y, meta, N, T, local, args.prefetch, args.prefetch_iters, h=run["h"],
+                                  sigma=run["sigma"], start=prefetch_auto["start_iteration"])
 
     configs = config_runs(ctx, args)
 
