@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define EPIPF_ABI_VERSION 7
+#define EPIPF_ABI_VERSION 8
 
 /* return codes */
 #define EPIPF_OK 0
@@ -96,6 +96,8 @@ typedef struct {
                                        weights (within the measured envelope of their error) could pick
                                        a neighbouring ancestor: a diagnostic count, always on; the draw itself is the
                                        numpy answer over the device's weights */
+    int64_t last_fused;          /* 1: the last epipf_run ran each chain's whole filter in one workgroup launch (N <= 256
+                                    with the lanes automatic); 0: one launch per filter step */
 } epipf_stats;
 
 /* groups: G for the subgroup models (1 <= G <= 4), ignored (1) for SIR/SEIR.

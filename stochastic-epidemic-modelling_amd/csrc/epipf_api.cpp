@@ -109,6 +109,7 @@ struct epipf_ctx {
     int lane_blocks = 1280;  // automatic choice: lane groups up to this many particle blocks per launch
     int group_block = 0;     // lane-group runs' particles per block: 0 = automatic (pick_block), 16 or 64 (EPIPF_GROUP_BLOCK)
     int xcd_map = 1;         // XCD-aware placement of the step launches' blocks (EPIPF_XCD_MAP=0: 2-D grid)
+    int fused = 1;           // one-workgroup filter for N <= kFusedMaxN when the lanes are automatic (EPIPF_FUSED=0: off)
     double split_p = -1.0;   // probs of the cached hi/lo split of log p, log1p(-p) (chains usually share probs)
     double split[4] = {0, 0, 0, 0};
 };
@@ -147,6 +148,34 @@ static int pick_block(const epipf_ctx* c, int W) {
     if (W < 8) return c->wg;
     if (c->group_block > 0) return c->group_block;
     return W >= 16 ? kGroupBlock : c->wg;
+}
+
+// Lanes per particle of the one-workgroup filter (epipf_fused.hpp), or 0 when the run takes the step launches: N <=
+// kFusedMaxN with the lanes automatic (an explicit epipf_set_lanes / EPIPF_LANES keeps the step kernels it names).  W is
+// the widest of 16 / 8 / 4 / 2 whose N W lanes fit one workgroup.
+static int pick_fused(const epipf_ctx* c) {
+    if (!c->fused || c->lanes > 0 || c->N > kFusedMaxN) return 0;
+    for (int W = 16; W > 2; W >>= 1)
+        if (c->N * W <= kFusedMaxThreads) return W;
+    return 2;
+}
+
+static hipError_t launch_fused_run(const StepArgs& a, const epipf_ctx* c, int obs, int n_chains, const FilterStreams& fs) {
+    const FusedFn f = fused_launcher(c->model, c->G, obs, a.lanes);
+    if (!f) return hipErrorInvalidValue;
+    const int threads = fused_threads_of(a.N, a.lanes);
+    const size_t lds = fused_lds_bytes_of(a.N, c->C, threads, a.fused_y ? a.T * c->K : 0,
+                                          a.fused_lf ? 2 * (a.lf_max + 1) : 0);
+    const hipStream_t s = fs.s[0];
+    if (fs.ev_init) (void)hipEventRecord(fs.ev_init, s);
+    if (fs.ev_step0) (void)hipEventRecord(fs.ev_step0, s);    // init runs inside the one launch: its time is in step_ms
+    if (fs.g_begin[0]) (void)hipEventRecord(fs.g_begin[0], s);
+    EPIPF_RANGE_PUSH("one-workgroup filter");
+    f(a, n_chains, threads, lds, s);
+    EPIPF_RANGE_POP();
+    if (fs.g_end[0]) (void)hipEventRecord(fs.g_end[0], s);
+    if (fs.ev_end) (void)hipEventRecord(fs.ev_end, s);
+    return hipGetLastError();
 }
 
 static int pick_lane_events(const epipf_ctx* c, int W) {
@@ -269,6 +298,7 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
         if (b == 0 || b == kGroupBlock || b == 64) c->group_block = b;
     }
     if (const char* e = getenv("EPIPF_XCD_MAP")) c->xcd_map = atoi(e) != 0;
+    if (const char* e = getenv("EPIPF_FUSED")) c->fused = atoi(e) != 0;
     c->B = (n_particles + c->wg - 1) / c->wg;
     if (step_lds_bytes(c->B, c->wg) > 160 * 1024) {
         free_ctx(c);
@@ -422,8 +452,9 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
 
     StepArgs a{};
     a.N = c->N; a.T = c->T; a.max_chains = c->max_chains;
-    a.lanes = pick_lanes(c, n_chains);
-    a.wg = pick_block(c, a.lanes);
+    const int fusedW = pick_fused(c);
+    a.lanes = fusedW ? fusedW : pick_lanes(c, n_chains);
+    a.wg = fusedW ? 64 : pick_block(c, a.lanes);
     a.B = (c->N + a.wg - 1) / a.wg;
     a.resample_mode = resample_mode; a.count_events = c->profiling >= EPIPF_PROFILE_COUNTERS ? 1 : 0; a.lf_max = c->lf_max;
     a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride; a.wstride = c->wstride; a.bstride = c->bstride;
@@ -434,7 +465,7 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     // is that layout's 64-blocks per lane, so the log-likelihood is the same whichever layout the chain count picks.
     const int B64 = (c->N + 63) / 64, S64 = prefix_segment(B64);
     a.canon_per = ((B64 + S64 - 1) / S64 + 63) / 64 * S64;
-    a.seg = (a.lanes > 1 && a.wg == kGroupBlock) ? (a.B <= kMaxFlatGroupBlocks ? 1 : 4 * S64) : prefix_segment(a.B);
+    a.seg = fusedW ? 1 : (a.lanes > 1 && a.wg == kGroupBlock) ? (a.B <= kMaxFlatGroupBlocks ? 1 : 4 * S64) : prefix_segment(a.B);
     a.nseg = (a.B + a.seg - 1) / a.seg;
     a.cert_k = cert_k(c->N, a.B, a.seg, 64);              // the block-sum scans run on 64 lanes whatever the layout
     // the reference-ambiguity test runs with the other device counters (bench.py's untimed counters iteration, the
@@ -449,12 +480,20 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
         return fail(EPIPF_EINVAL, "no lane-group kernel for %d lanes x %d events", a.lanes, a.lane_events);
     c->stats.last_lanes = a.lanes;
     c->stats.last_lane_events = a.lane_events;
+    c->stats.last_fused = fusedW ? 1 : 0;
+    if (fusedW) {   // stage Y, then the log n! table, in LDS while the launch stays within the default dynamic LDS limit
+        const int threads = fused_threads_of(a.N, a.lanes);
+        const size_t base = fused_lds_bytes_of(a.N, c->C, threads, 0, 0);
+        const size_t yb = sizeof(double) * (size_t)a.T * c->K, lb = sizeof(double) * 2 * (size_t)(a.lf_max + 1);
+        a.fused_y = base + yb <= kFusedLdsLimit;
+        a.fused_lf = a.lf_max >= 0 && base + (a.fused_y ? yb : 0) + lb <= kFusedLdsLimit;
+    }
     for (int g = 0; g < kMaxG; ++g) { a.npop[g] = c->npop[g]; a.mu[g] = c->mu[g]; a.emu[g] = c->emu[g]; a.kmax[g] = c->kmax[g]; }
 
     EPIPF_RANGE_PUSH("epipf_run");
     struct RangeEnd { ~RangeEnd() { EPIPF_RANGE_POP(); } } range_end;
     FilterStreams fs{};
-    fs.n = std::min(c->n_streams, n_chains);
+    fs.n = fusedW ? 1 : std::min(c->n_streams, n_chains);
     // Created on first use, not with the context: HIP maps streams onto its few hardware queues in creation order,
     // so contexts that each run one group (run_pipelined) get one stream each and land on different queues.
     if (!ensure_streams(c, fs.n)) return fail(EPIPF_EHIP, "auxiliary stream creation failed");
@@ -473,7 +512,8 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
         fs.g_end[g] = c->profiling ? c->ge[g] : nullptr;
     }
     c->last_groups = fs.n;
-    hipError_t le = launch_filter(a, c->model, c->G, obs_model, n_chains, fs);
+    hipError_t le = fusedW ? launch_fused_run(a, c, obs_model, n_chains, fs)
+                           : launch_filter(a, c->model, c->G, obs_model, n_chains, fs);
     if (le != hipSuccess) return fail(EPIPF_EHIP, "kernel launch failed: %s", hipGetErrorString(le));
     HIP_TRY(hipMemcpyAsync(c->h_status, c->status, sizeof(int32_t) * n_chains, hipMemcpyDeviceToHost, c->stream));
     if (log_zetas_out)
@@ -503,12 +543,12 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
         c->stats.init_ms += ms_init;
         c->stats.init_launches += 1;
         c->stats.step_ms += ms_step;
-        c->stats.step_launches += c->T - 1;
+        c->stats.step_launches += fusedW ? 1 : c->T - 1;   // the one-workgroup filter: one launch per run
         for (int g = 0; g < c->last_groups; ++g) {        // each group's back-to-back step kernels on its stream
             float ms_g = 0.f;
             HIP_TRY(hipEventElapsedTime(&ms_g, c->gb[g], c->ge[g]));
             c->stats.step_kernel_ms += ms_g;
-            c->stats.step_kernel_launches += c->T - 1;
+            c->stats.step_kernel_launches += fusedW ? 1 : c->T - 1;
         }
     }
     unsigned long long tot[kNumCounters] = {};

@@ -66,6 +66,7 @@ struct StepArgs {
                                    // (summed on the host)
     double npop[kMaxG], mu[kMaxG], emu[kMaxG];
     int kmax[kMaxG];
+    int fused_y, fused_lf;        // one-workgroup filter: Y / the log n! table staged in LDS (epipf_fused.hpp)
 };
 
 struct PathArgs {
@@ -193,6 +194,15 @@ constexpr int kMaxSegments = 200;
 constexpr int kMaxFlatGroupBlocks = 1280;
 constexpr int kGroupBlock = 16;   // particles per block of the lane-group runs that spread a chain over every CU
 hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_chains, const FilterStreams& fs);
+// the one-workgroup filter (epipf_fused.hpp): init and every step of a chain in one launch, for N <= kFusedMaxN;
+// one workgroup of fused_threads(N, W) threads per chain, W lanes per particle in the SSA
+constexpr int kFusedMaxThreads = 512;    // 8 waves: up to 256 VGPRs a lane (2 waves per SIMD)
+constexpr int kFusedMaxN = 256;
+constexpr size_t kFusedLdsLimit = 64 * 1024;    // the default dynamic LDS limit of a launch
+using FusedFn = void (*)(const StepArgs& a, int n_chains, int threads, size_t lds, hipStream_t s);
+FusedFn fused_launcher(int model, int G, int obs, int W);
+size_t fused_lds_bytes_of(int N, int C, int threads, int TK, int lf_n);   // TK / lf_n: doubles staged (0: none)
+int fused_threads_of(int N, int W);
 hipError_t launch_path_sample(const PathArgs& a, hipStream_t s);
 hipError_t launch_simulate(const SimArgs& a, int model, int G, hipStream_t s);
 hipError_t launch_simulate_path(const SimPathArgs& a, int model, int G, hipStream_t s);

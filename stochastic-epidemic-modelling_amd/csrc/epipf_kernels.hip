@@ -42,19 +42,7 @@ __global__ __launch_bounds__(WG) void pf_init_kernel(StepArgs a) {
 #pragma unroll
     for (int c = 0; c < C; ++c) x[c] = 0.0;
     if (mine && j < a.N) {
-#pragma unroll
-        for (int g = 0; g < ((MODEL >= kSubgroups) ? G : 1); ++g) {
-            const Block r = philox((uint32_t)g, (uint32_t)j, kDomainInit, cp.f, cp.k0, cp.k1);
-            const double U = u01(r.x, r.y);
-            const double mu = a.mu[g];
-            double pk = a.emu[g], F = pk;
-            int k = 0;
-            while (U >= F && k < a.kmax[g]) { k += 1; pk = pk * mu / (double)k; F = F + pk; }
-            const double S0 = a.npop[g] - (double)k;
-            if constexpr (MODEL == kSIR) { x[0] = S0; x[1] = (double)k; }
-            else if constexpr (MODEL == kSEIR) { x[0] = S0; x[2] = (double)k; }
-            else { x[3 * g] = S0; x[3 * g + 1] = (double)k; }
-        }
+        init_particle<MODEL, G>(a, cp, j, x);                  // pmcmc.py:156-175
         int32_t* h = a.hidden + (size_t)chain * a.hist_stride + (size_t)j * C;
 #pragma unroll
         for (int c = 0; c < C; ++c) h[c] = (int32_t)x[c];

@@ -25,6 +25,29 @@ __device__ __forceinline__ BlockPos step_block(const StepArgs& a) {
     return {a.chain0 + c, L - c * a.B};
 }
 
+// Initial state of particle j (pmcmc.py:156-175): per group an initial infected count Poisson(mu) by CDF inversion on
+// the keyed stream (counter (g, j, 2 << 24, f)), S = population - I, the rest 0.  pf_init_kernel and the one-workgroup
+// filter (epipf_fused.hpp) draw it with this code.
+template <int MODEL, int G>
+__device__ __forceinline__ void init_particle(const StepArgs& a, const ChainParam& cp, int j, double* x) {
+    constexpr int C = Shape<MODEL, G>::C;
+#pragma unroll
+    for (int c = 0; c < C; ++c) x[c] = 0.0;
+#pragma unroll
+    for (int g = 0; g < ((MODEL >= kSubgroups) ? G : 1); ++g) {
+        const Block r = philox((uint32_t)g, (uint32_t)j, kDomainInit, cp.f, cp.k0, cp.k1);
+        const double U = u01(r.x, r.y);
+        const double mu = a.mu[g];
+        double pk = a.emu[g], F = pk;
+        int k = 0;
+        while (U >= F && k < a.kmax[g]) { k += 1; pk = pk * mu / (double)k; F = F + pk; }
+        const double S0 = a.npop[g] - (double)k;
+        if constexpr (MODEL == kSIR) { x[0] = S0; x[1] = (double)k; }
+        else if constexpr (MODEL == kSEIR) { x[0] = S0; x[2] = (double)k; }
+        else { x[3 * g] = S0; x[3 * g + 1] = (double)k; }
+    }
+}
+
 // LDS ordering between the lanes that run a helper: the whole block (__syncthreads), or only the calling wave
 // (WAVE = true: the lane-group kernel runs these on its first wave while the other waves wait at a block barrier).
 template <bool WAVE>

@@ -16,7 +16,7 @@ SIR, SEIR, SIR_SUBGROUPS, SIR_SUBGROUPS2 = 0, 1, 2, 3
 OBS_BINOMIAL, OBS_NORMAL = 0, 1
 RESAMPLE_MULTINOMIAL, RESAMPLE_SYSTEMATIC = 0, 1
 PROFILE_OFF, PROFILE_TIMING, PROFILE_COUNTERS = 0, 1, 2
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 EXPORTS = (
     "epipf_create", "epipf_destroy", "epipf_set_observations", "epipf_set_population", "epipf_run",
@@ -49,6 +49,7 @@ class Stats(ctypes.Structure):
         ("last_lanes", ctypes.c_int64),
         ("last_lane_events", ctypes.c_int64),
         ("resample_ref_ambiguous", ctypes.c_int64),
+        ("last_fused", ctypes.c_int64),
     ]
 
     def as_dict(self):

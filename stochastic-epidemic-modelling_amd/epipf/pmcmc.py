@@ -157,6 +157,36 @@ def mvn_apply(z, fac, mean):
     return x.reshape(fac.shape[0])
 
 
+def _raw_words(rng):
+    """The MT19937 bit generator behind a legacy RandomState (or the np.random module's global one), else None."""
+    if rng is np.random:
+        rng = np.random.mtrand._rand
+    if type(rng) is np.random.RandomState:
+        bg = rng._bit_generator
+        if type(bg) is np.random.MT19937:
+            return bg
+    return None
+
+
+def legacy_randint(rng, n, bg=None):
+    """rng.randint(0, n) for 1 <= n <= 2^32 with the same value and the same stream consumption: numpy's legacy
+    bounded draw is masked rejection on 32-bit MT19937 words (v = next32 & mask until v <= n - 1), which is what the
+    bit generator's random_raw() returns one at a time -- without randint's argument handling (~2.9 -> ~1.1 us).
+    bg: _raw_words(rng), when the caller has it; other generators fall back to rng.randint."""
+    if bg is None:
+        bg = _raw_words(rng)
+        if bg is None:
+            return int(rng.randint(0, n))
+    r = int(n) - 1
+    if r <= 0:
+        return 0
+    mask = (1 << r.bit_length()) - 1
+    while True:
+        v = bg.random_raw() & mask
+        if v <= r:
+            return int(v)
+
+
 def _log_ratio(lz_new, lz_old):
     """Underflow-free MH acceptance probability min(1, z'/z) from log-likelihoods (the symmetric
     Gaussian proposal terms of pmcmc.py:380-391 cancel)."""
@@ -242,6 +272,11 @@ class ChainSampler:
         self._fac = [None] * nc                                  # multivariate_normal factor of h * std[c]
         self.fnext = [int(filter_index_start)] * nc
         self.filters_run = [0] * nc
+        # per-chain host RNG entry points, looked up once (a step makes 3 calls per chain)
+        self._normal = [r.standard_normal for r in self.rngs]
+        self._uniform = [r.random_sample for r in self.rngs]
+        self._raw = [_raw_words(r) for r in self.rngs]
+        self._dbuf = np.empty((nc, d))
         self.acceptances = [1] * nc
         self.dth = d - (1 if probs is None else 0)
         self.i = 0
@@ -293,8 +328,9 @@ class ChainSampler:
 
     def _path_sample(self, ok):
         chosen = np.zeros(self.nc, dtype=np.int32)
+        N, rngs, raw = self.N, self.rngs, self._raw
         for c in ok:
-            chosen[c] = self.rngs[c].randint(0, self.N)            # pmcmc.py:241, host RNG order kept
+            chosen[c] = legacy_randint(rngs[c], N, raw[c])          # pmcmc.py:241, host RNG order kept
         return self.eng.path_sample(chosen)
 
     def _copy_prev(self, c, i):
@@ -337,12 +373,19 @@ class ChainSampler:
         of the previous row -- is one array operation over the chains."""
         i = self.i
         nc, d = self.nc, self.d
-        P = np.empty((nc, d))
-        for c in range(nc):
-            if self.adaptive and i > 1e3:
+        if self.adaptive and i > 1e3:
+            for c in range(nc):
                 self.std[c] = np.cov(self.thetas[c, :i].T, ddof=0) + 1e-4 * np.eye(self.d)
                 self._fac[c] = None
-            P[c] = self._propose(c, self.thetas[c, i - 1])
+        # multivariate_normal(theta, h std) per chain (mvn_apply's arithmetic: np.dot(z, factor) per chain -- a
+        # batched product would take another BLAS kernel and round differently -- then + theta for all chains)
+        D, fac, normal = self._dbuf, self._fac, self._normal
+        for c in range(nc):
+            f = fac[c]
+            if f is None:
+                f = fac[c] = mvn_factor(self.h * self.std[c])
+            np.dot(normal[c](d).reshape(1, d), f, out=D[c:c + 1])
+        P = D + self.thetas[:, i - 1]
         live = ~(P < 0).any(axis=1)                               # sum(prop < 0) > 0: no filter, :333-337
         lv = np.flatnonzero(live)
         acc = np.zeros(0, dtype=np.intp)
@@ -363,18 +406,25 @@ class ChainSampler:
             self.last_active = int(lv.size)
             ok = np.flatnonzero(live & (st == _lib.STATUS_OK))    # degenerate filters: rejected, :365-369
             if ok.size:
-                tr = self._path_sample(ok.tolist())
+                okl = ok.tolist()
+                tr = self._path_sample(okl)
                 lzT = lz[:, -1]
                 take = []
-                for c in ok.tolist():
-                    if self.mh_ratio == "reference":
+                uniform = self._uniform
+                if self.mh_ratio == "reference":
+                    for c in okl:
                         prob = _reference_ratio(np.exp(lzT[c]), self.likelihoods[c, i - 1], new_all[c],
                                                 self.thetas[c, i - 1], self.params[c], self.h * self.std[c])
-                    else:
-                        prob = _log_ratio(lzT[c], self.loglik[c, i - 1])
-                    if self.rngs[c].random_sample() < prob:        # == uniform(): 0 + 1*U, 7x cheaper
-                        take.append(c)
-                        self.acceptances[c] += 1
+                        if uniform[c]() < prob:                    # == uniform(): 0 + 1*U, 7x cheaper
+                            take.append(c)
+                else:                                              # _log_ratio, the differences for all chains at once
+                    exp, isnan = math.exp, math.isnan
+                    for c, lr in zip(okl, (lzT[ok] - self.loglik[ok, i - 1]).tolist()):
+                        prob = 0.0 if isnan(lr) else min(1.0, exp(min(lr, 0.0)))
+                        if uniform[c]() < prob:
+                            take.append(c)
+                for c in take:
+                    self.acceptances[c] += 1
                 if take:
                     acc = np.asarray(take, dtype=np.intp)
                     self.thetas[acc, i] = new_all[acc]
