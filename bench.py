@@ -305,7 +305,11 @@ def timed_chains(ctx, args, cfg, chains, steps, warmup, kind, pipelines=1, strea
     cst = stats_sum()
     dt_max, filters_all = ctx.max_sum(dt, filters)
     lanes = int(engines[0].stats()["last_lanes"]) or 1
+    fused = int(engines[0].stats().get("last_fused", 0))
+    if fused:                                      # one launch per filter batch, one stream per engine
+        streams = P
     return dict(Y=Y, meta=meta, N=N, T=T, chains=chains, P=P, streams=streams, samplers=samplers, engines=engines,
+                fused=fused,
                 dt=dt_max, filters=filters, filters_all=filters_all, value=filters_all * N * T / dt_max, st=st, cst=cst,
                 lanes=lanes, h=h, sigma=sigma, proposal=pdesc, gathered=gathered,
                 acceptance_rate=(a1 - a0) / max(1, f1 - f0), steps=steps, warmup=warmup)
@@ -345,7 +349,9 @@ def roofline(run, value):
     launches = max(1, st["step_kernel_launches"])
     avg_launch_s = st["step_kernel_ms"] / 1e3 / launches
     step_wall_s = st["step_ms"] / 1e3 / max(1, st["step_launches"])
-    units_per_launch = run["filters"] * N / steps / run["streams"]   # particle-steps per kernel launch
+    # particle-steps per kernel launch: one filter step of a chain group, or (the one-workgroup filter) every step of
+    # an engine's chains
+    units_per_launch = run["filters"] * N / steps / run["streams"] * (run["T"] if run.get("fused") else 1)
     bytes_per_unit = 8 * n_comp(meta) + 40                            # 8C+40 B per particle-step
     live_gbs = units_per_launch * bytes_per_unit / avg_launch_s / 1e9
     # chip level: algorithmic bytes of every particle-step of the timed region over its wall time
@@ -378,8 +384,7 @@ def roofline(run, value):
            else "HIP events (launch to completion)",
            "frac_hip_event_span": live_gbs / HBM_PEAK_GBS, "chip_level_frac": chip_gbs / HBM_PEAK_GBS,
            "bytes_per_particle_step": bytes_per_unit, "traffic": traffic, "traffic_raw": traffic_raw}
-    kernel = "pf_step_kernel" if lanes == 1 else f"pf_step_group_kernel (W={lanes})"
-    return {"bound": "valu", "kernel": kernel,
+    return {"bound": "valu", "kernel": kernel_name(run),
             "achieved": valu["achieved"] if valu else None, "peak": VALU_PEAK,
             "unit": "wave64 VALU instr/s", "frac": valu["achieved"] / VALU_PEAK if valu else None,
             "traffic": traffic, "valu_issue": valu, "hbm": hbm,
@@ -391,13 +396,19 @@ def roofline(run, value):
             "pmc_profile": {"path": pmc_path, "build_id": pmc.get("build_id")}}
 
 
+def kernel_name(run):
+    if run.get("fused"):
+        return f"pf_filter_wg_kernel (one workgroup per chain, W={run['lanes']})"
+    return "pf_step_kernel" if run["lanes"] == 1 else f"pf_step_group_kernel (W={run['lanes']})"
+
+
 def run_summary(run):
     cst = run["cst"]
     ps = cst["particle_steps"]
     return {"value": run["value"], "unit": "particle-steps/s", "ms_per_step": run["dt"] * 1e3 / run["steps"],
             "steps": run["steps"], "warmup": run["warmup"], "chains_per_gpu": run["chains"],
             "particles": run["N"], "T_obs": run["T"], "lanes_per_particle": run["lanes"],
-            "kernel": "pf_step_kernel" if run["lanes"] == 1 else "pf_step_group_kernel",
+            "kernel": kernel_name(run),
             "h": run["h"], "proposal": run["proposal"], "acceptance_rate": run["acceptance_rate"],
             "events_per_particle_step": cst["events"] / ps if ps else None,
             "events_per_s": run["value"] * cst["events"] / ps if ps else None}
@@ -456,8 +467,11 @@ def config_runs(ctx, args):
         if cfg == 1:
             steps *= 10                                                # 2-3 ms MH steps: time a few hundred ms
         entry = None
+        # N <= 256 (config 1): the engine's first six runs of a batch size time the one-workgroup filter against the
+        # step launches (EPIPF_FUSED=auto, epipf_api.cpp): warm up past them
+        warm = 8 if mc["N"] <= 256 else (1 if chains > 1 else 2)
         for kind in ("config", "fixed_theta"):
-            run = timed_chains(ctx, args, cfg, chains, steps, 1 if chains > 1 else 2, kind, pipelines=pipelines)
+            run = timed_chains(ctx, args, cfg, chains, steps, warm, kind, pipelines=pipelines)
             run["cfg"] = cfg
             if entry is None:
                 entry = run_summary(run)

@@ -123,6 +123,17 @@ int epipf_run(epipf_ctx* ctx, int n_chains, const double* theta, int d, int obs_
               const uint64_t* keys, const uint32_t* filter_index, const int32_t* active, int resample_mode,
               double* log_zetas_out, int32_t* status_out);
 
+/* epipf_run, then the path sampler of epipf_path_sample on the same stream before the results come back: one round
+ * trip per MH iteration instead of two (pmcmc.py:360-362 -- particle_filter, then particle_path_sampler).
+ *   chosen [n_chains]: the final particle of each chain's sampled path (the host's np.random.randint(0, N) draw,
+ *                      taken before the filter -- epipf.pmcmc peeks it off the RandomState without consuming it),
+ *                      or -1 for none
+ *   traj_out [n_chains*T*C] int32: the sampled trajectories; zeros for chains with chosen -1 or a status other than
+ *                      EPIPF_STATUS_OK (the reference draws no path after a degenerate filter) */
+int epipf_run_sampled(epipf_ctx* ctx, int n_chains, const double* theta, int d, int obs_model, const double* probs,
+                      const uint64_t* keys, const uint32_t* filter_index, const int32_t* active, int resample_mode,
+                      const int32_t* chosen, double* log_zetas_out, int32_t* status_out, int32_t* traj_out);
+
 /* Copy the last run's history: hidden [n_chains*T*N*C] int32 (compartment counts), ancestry [n_chains*T*N]
  * int32 (row 0 zeros, as pmcmc.py:152).  Either pointer may be NULL. */
 int epipf_copy_history(epipf_ctx* ctx, int n_chains, int32_t* hidden_out, int32_t* ancestry_out);

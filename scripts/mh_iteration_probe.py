@@ -21,10 +21,11 @@ ap.add_argument("--chains", type=int, default=1)
 ap.add_argument("--iters", type=int, default=200)
 ap.add_argument("--h", type=float, default=1e-4)
 ap.add_argument("--tag", default="")
+ap.add_argument("--particles", type=int, default=0, help="override the config's N")
 args = ap.parse_args()
 
 Y, meta = datasets.benchmark_dataset(args.cfg)
-N, T = meta["N"], Y.shape[0]
+N, T = (args.particles or meta["N"]), Y.shape[0]
 nc = args.chains
 s = ChainSampler(Y, meta["model"], list(meta["theta"]), args.h, sigma=meta["sigma"], iters=2 * args.iters + 10,
                  observations=meta.get("observations", False), probs=meta["probs"], n_particles=N,

@@ -7,11 +7,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -64,6 +66,12 @@ struct epipf_ctx {
     hipStream_t stream = nullptr;
     size_t hist_stride = 0, anc_stride = 0, wstride = 0, bstride = 0;
     int32_t *hidden = nullptr, *ancestry = nullptr, *status = nullptr, *chosen = nullptr, *traj = nullptr;
+    // status [max_chains] | counters | log_zeta [max_chains][t_max] in one block (device and pinned host), so that a
+    // run's results come back in one copy; status, counters and log_zeta point into it
+    void* res = nullptr;
+    void* h_res = nullptr;
+    size_t res_counters = 0, res_lz = 0;   // byte offsets of counters and log_zeta in the block
+    int32_t* h_traj = nullptr;             // pinned staging of epipf_run_sampled's trajectories
     double *wraw = nullptr, *wloc = nullptr, *bsum = nullptr, *log_zeta = nullptr, *Y = nullptr, *lf = nullptr;
     ChainParam* cp = nullptr;
     LogTab* logtab = nullptr;
@@ -109,7 +117,21 @@ struct epipf_ctx {
     int lane_blocks = 1280;  // automatic choice: lane groups up to this many particle blocks per launch
     int group_block = 0;     // lane-group runs' particles per block: 0 = automatic (pick_block), 16 or 64 (EPIPF_GROUP_BLOCK)
     int xcd_map = 1;         // XCD-aware placement of the step launches' blocks (EPIPF_XCD_MAP=0: 2-D grid)
-    int fused = 1;           // one-workgroup filter for N <= kFusedMaxN when the lanes are automatic (EPIPF_FUSED=0: off)
+    // one-workgroup filter for N <= kFusedMaxN when the lanes are automatic: -1 = measured per batch size (FusedTune),
+    // 1 = always, 0 = never (EPIPF_FUSED)
+    int fused = -1;
+    int fused_lanes = 0;     // its SSA lanes per particle: 0 = automatic (pick_fused), EPIPF_FUSED_LANES = 1/2/4/8/16
+    // Which path is faster depends on the events per particle-step, which the host cannot see ahead: one workgroup per
+    // chain wins where a step is little work or many chains fill the chip (config 1, N = 100, 6 events: 3.1x at 256
+    // chains, 1.3x at one), the step launches where one chain's many events want more than one CU (N = 100 at config
+    // 2's 90 events: 2.2x the other way).  So a batch size's first runs time both (wall clock of epipf_run, results
+    // identical either way) and the faster one stays.
+    struct FusedTune {
+        int runs = 0;
+        double best[2] = {1e300, 1e300};   // fastest timed run: [0] step launches, [1] one-workgroup filter
+        int choice = -1;
+    };
+    std::map<int, FusedTune> fused_tune;   // by n_chains
     double split_p = -1.0;   // probs of the cached hi/lo split of log p, log1p(-p) (chains usually share probs)
     double split[4] = {0, 0, 0, 0};
 };
@@ -155,9 +177,25 @@ static int pick_block(const epipf_ctx* c, int W) {
 // the widest of 16 / 8 / 4 / 2 whose N W lanes fit one workgroup.
 static int pick_fused(const epipf_ctx* c) {
     if (!c->fused || c->lanes > 0 || c->N > kFusedMaxN) return 0;
-    for (int W = 16; W > 2; W >>= 1)
-        if (c->N * W <= kFusedMaxThreads) return W;
-    return 2;
+    if (c->fused_lanes > 0 && c->N * c->fused_lanes <= kFusedMaxThreads) return c->fused_lanes;
+    return 1;
+}
+
+// EPIPF_FUSED=auto (the default): runs 0-3 of a batch size alternate the paths (fused first, each path's first run
+// untimed), then the faster one's fastest timed run decides.  *timed: this run's wall time is recorded.
+static bool fused_decide(epipf_ctx* c, int n_chains, bool& timed) {
+    timed = false;
+    if (c->fused >= 0) return c->fused == 1;
+    epipf_ctx::FusedTune& t = c->fused_tune[n_chains];
+    if (t.choice >= 0) return t.choice == 1;
+    timed = t.runs >= 2;                                 // runs 0, 1: warm-up of each path
+    return (t.runs & 1) == 0;                            // even runs: fused
+}
+
+static void fused_record(epipf_ctx* c, int n_chains, bool fused, double seconds) {
+    epipf_ctx::FusedTune& t = c->fused_tune[n_chains];
+    t.best[fused ? 1 : 0] = std::min(t.best[fused ? 1 : 0], seconds);
+    if (++t.runs >= 6) t.choice = t.best[1] <= t.best[0] ? 1 : 0;
 }
 
 static hipError_t launch_fused_run(const StepArgs& a, const epipf_ctx* c, int obs, int n_chains, const FilterStreams& fs) {
@@ -210,11 +248,11 @@ static void free_ctx(epipf_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    void* dev[] = {c->hidden, c->ancestry, c->status, c->chosen, c->traj, c->wraw, c->wloc, c->bsum,
-                   c->log_zeta, c->Y, c->lf, c->cp, c->logtab, c->counters, c->scratch, c->abc};
+    void* dev[] = {c->hidden, c->ancestry, c->res, c->chosen, c->traj, c->wraw, c->wloc, c->bsum,
+                   c->Y, c->lf, c->cp, c->logtab, c->scratch, c->abc};
     for (void* p : dev)
         if (p) (void)hipFree(p);
-    void* host[] = {c->h_cp, c->h_status, c->h_lz, c->h_counters};
+    void* host[] = {c->h_cp, c->h_res, c->h_traj};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
     for (auto& e : c->ev)
@@ -248,6 +286,8 @@ extern "C" {
 
 const char* epipf_last_error(void) { return g_err.c_str(); }
 int epipf_abi_version(void) { return EPIPF_ABI_VERSION; }
+static_assert(kStatusOk == EPIPF_STATUS_OK && kStatusDegenerate == EPIPF_STATUS_DEGENERATE &&
+              kStatusSkipped == EPIPF_STATUS_SKIPPED, "device status codes");
 const char* epipf_build_id(void) {
 #ifdef EPIPF_BUILD_ID
     return EPIPF_BUILD_ID;
@@ -298,7 +338,11 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
         if (b == 0 || b == kGroupBlock || b == 64) c->group_block = b;
     }
     if (const char* e = getenv("EPIPF_XCD_MAP")) c->xcd_map = atoi(e) != 0;
-    if (const char* e = getenv("EPIPF_FUSED")) c->fused = atoi(e) != 0;
+    if (const char* e = getenv("EPIPF_FUSED")) c->fused = strcmp(e, "auto") == 0 ? -1 : atoi(e) != 0;
+    if (const char* e = getenv("EPIPF_FUSED_LANES")) {
+        const int w = atoi(e);
+        if (w == 0 || w == 1 || w == 2 || w == 4 || w == 8 || w == 16) c->fused_lanes = w;
+    }
     c->B = (n_particles + c->wg - 1) / c->wg;
     if (step_lds_bytes(c->B, c->wg) > 160 * 1024) {
         free_ctx(c);
@@ -317,24 +361,30 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
     }
     rc |= dalloc(&c->hidden, (size_t)max_chains * c->hist_stride);
     rc |= dalloc(&c->ancestry, (size_t)max_chains * c->anc_stride);
-    rc |= dalloc(&c->status, (size_t)max_chains);
+    c->res_counters = ((sizeof(int32_t) * (size_t)max_chains + 127) / 128) * 128;
+    c->res_lz = c->res_counters + sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride;
+    const size_t res_bytes = c->res_lz + sizeof(double) * (size_t)max_chains * t_max;
+    rc |= dalloc(reinterpret_cast<char**>(&c->res), res_bytes);
     rc |= dalloc(&c->chosen, (size_t)max_chains);
     rc |= dalloc(&c->traj, (size_t)max_chains * t_max * c->C);
     rc |= dalloc(&c->wraw, 2 * (size_t)max_chains * c->wstride);
     rc |= dalloc(&c->wloc, 2 * (size_t)max_chains * c->wstride);
     rc |= dalloc(&c->bsum, 2 * (size_t)max_chains * c->bstride);
-    rc |= dalloc(&c->log_zeta, (size_t)max_chains * t_max);
     rc |= dalloc(&c->cp, (size_t)max_chains);
     rc |= dalloc(&c->logtab, (size_t)kLogTabEntries);
-    rc |= dalloc(&c->counters, (size_t)kCounterSlots * kCounterStride);
     if (rc) { free_ctx(c); return EPIPF_ENOMEM; }
+    c->status = static_cast<int32_t*>(c->res);
+    c->counters = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->res) + c->res_counters);
+    c->log_zeta = reinterpret_cast<double*>(static_cast<char*>(c->res) + c->res_lz);
     if (hipHostMalloc((void**)&c->h_cp, sizeof(ChainParam) * max_chains) != hipSuccess ||
-        hipHostMalloc((void**)&c->h_status, sizeof(int32_t) * max_chains) != hipSuccess ||
-        hipHostMalloc((void**)&c->h_lz, sizeof(double) * (size_t)max_chains * t_max) != hipSuccess ||
-        hipHostMalloc((void**)&c->h_counters, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride) != hipSuccess) {
+        hipHostMalloc(&c->h_res, res_bytes) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_traj, sizeof(int32_t) * (size_t)max_chains * t_max * c->C) != hipSuccess) {
         free_ctx(c);
         return fail(EPIPF_ENOMEM, "hipHostMalloc failed");
     }
+    c->h_status = static_cast<int32_t*>(c->h_res);
+    c->h_counters = reinterpret_cast<unsigned long long*>(static_cast<char*>(c->h_res) + c->res_counters);
+    c->h_lz = reinterpret_cast<double*>(static_cast<char*>(c->h_res) + c->res_lz);
     for (auto& e : c->ev)
         if (hipEventCreate(&e) != hipSuccess) { free_ctx(c); return fail(EPIPF_EHIP, "hipEventCreate failed"); }
     if (hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess) {
@@ -403,10 +453,11 @@ int epipf_set_population(epipf_ctx* c, const double* n_population, const double*
     return EPIPF_OK;
 }
 
-int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_model, const double* probs,
-              const uint64_t* keys, const uint32_t* filter_index, const int32_t* active, int resample_mode,
-              double* log_zetas_out, int32_t* status_out) {
+static int run_impl(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_model, const double* probs,
+                    const uint64_t* keys, const uint32_t* filter_index, const int32_t* active, int resample_mode,
+                    const int32_t* chosen, double* log_zetas_out, int32_t* status_out, int32_t* traj_out) {
     if (!c || !theta || !probs || !keys || !filter_index || !status_out) return fail(EPIPF_EINVAL, "NULL argument");
+    if ((chosen == nullptr) != (traj_out == nullptr)) return fail(EPIPF_EINVAL, "chosen and traj_out go together");
     if (!c->have_Y) return fail(EPIPF_ESTATE, "epipf_set_observations was not called");
     if (!c->have_pop) return fail(EPIPF_ESTATE, "epipf_set_population was not called");
     if (n_chains < 1 || n_chains > c->max_chains) return fail(EPIPF_EINVAL, "n_chains=%d outside [1, %d]", n_chains, c->max_chains);
@@ -443,16 +494,23 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
         q.flags = (c->fast_ssa ? kChainFastSsa : 0u) | (c->seq_decide ? kChainSeqDecide : 0u);
         q.clock_slack = c->clock_slack;
         q.band_slack = c->band_slack;
-        c->h_status[ch] = on ? EPIPF_STATUS_OK : EPIPF_STATUS_SKIPPED;
+        q.skip = on ? 0 : 1;                            // the first kernel writes the chain's status from it
+        q.chosen = -1;
+        if (chosen && on) {
+            if (chosen[ch] >= c->N) return fail(EPIPF_EINVAL, "chosen[%d]=%d outside [0, N)", ch, chosen[ch]);
+            q.chosen = chosen[ch] < 0 ? -1 : chosen[ch];
+        }
         n_active += on;
     }
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemcpyAsync(c->cp, c->h_cp, sizeof(ChainParam) * n_chains, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->status, c->h_status, sizeof(int32_t) * n_chains, hipMemcpyHostToDevice, c->stream));
 
     StepArgs a{};
     a.N = c->N; a.T = c->T; a.max_chains = c->max_chains;
-    const int fusedW = pick_fused(c);
+    bool tune_timed = false;
+    const int fusedW = pick_fused(c) && fused_decide(c, n_chains, tune_timed) ? pick_fused(c) : 0;
+    const bool tuning = pick_fused(c) && c->fused < 0 && c->fused_tune[n_chains].choice < 0;
+    const auto t_start = std::chrono::steady_clock::now();
     a.lanes = fusedW ? fusedW : pick_lanes(c, n_chains);
     a.wg = fusedW ? 64 : pick_block(c, a.lanes);
     a.B = (c->N + a.wg - 1) / a.wg;
@@ -515,12 +573,26 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     hipError_t le = fusedW ? launch_fused_run(a, c, obs_model, n_chains, fs)
                            : launch_filter(a, c->model, c->G, obs_model, n_chains, fs);
     if (le != hipSuccess) return fail(EPIPF_EHIP, "kernel launch failed: %s", hipGetErrorString(le));
-    HIP_TRY(hipMemcpyAsync(c->h_status, c->status, sizeof(int32_t) * n_chains, hipMemcpyDeviceToHost, c->stream));
-    if (log_zetas_out)
-        HIP_TRY(hipMemcpyAsync(c->h_lz, c->log_zeta, sizeof(double) * (size_t)n_chains * c->T, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->h_counters, c->counters, sizeof(unsigned long long) * (size_t)kCounterSlots * kCounterStride, hipMemcpyDeviceToHost,
+    if (chosen) {   // the path sampler (pmcmc.py:236-248) after the filter, on the same stream: no second round trip
+        PathArgs pa{};
+        pa.n_chains = n_chains; pa.N = c->N; pa.T = c->T; pa.C = c->C;
+        pa.hist_stride = c->hist_stride; pa.anc_stride = c->anc_stride;
+        pa.hidden = c->hidden; pa.ancestry = c->ancestry; pa.chosen = nullptr; pa.cp = c->cp; pa.status = c->status;
+        pa.traj = c->traj;
+        hipError_t pe = launch_path_sample(pa, c->stream);
+        if (pe != hipSuccess) return fail(EPIPF_EHIP, "path kernel launch failed: %s", hipGetErrorString(pe));
+        HIP_TRY(hipMemcpyAsync(c->h_traj, c->traj, sizeof(int32_t) * (size_t)n_chains * c->T * c->C,
+                               hipMemcpyDeviceToHost, c->stream));
+    }
+    // status, counters and the log-likelihoods: one copy of the result block's prefix
+    HIP_TRY(hipMemcpyAsync(c->h_res, c->res, c->res_lz + sizeof(double) * (size_t)n_chains * c->T, hipMemcpyDeviceToHost,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (tuning) {
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+        fused_record(c, n_chains, fusedW != 0, tune_timed ? dt : 1e300);
+    }
+    if (chosen) memcpy(traj_out, c->h_traj, sizeof(int32_t) * (size_t)n_chains * c->T * c->C);
     memcpy(status_out, c->h_status, sizeof(int32_t) * n_chains);
     if (log_zetas_out) {
         memcpy(log_zetas_out, c->h_lz, sizeof(double) * (size_t)n_chains * c->T);
@@ -569,6 +641,21 @@ int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_mo
     return EPIPF_OK;
 }
 
+int epipf_run(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_model, const double* probs,
+              const uint64_t* keys, const uint32_t* filter_index, const int32_t* active, int resample_mode,
+              double* log_zetas_out, int32_t* status_out) {
+    return run_impl(c, n_chains, theta, d, obs_model, probs, keys, filter_index, active, resample_mode, nullptr,
+                    log_zetas_out, status_out, nullptr);
+}
+
+int epipf_run_sampled(epipf_ctx* c, int n_chains, const double* theta, int d, int obs_model, const double* probs,
+                      const uint64_t* keys, const uint32_t* filter_index, const int32_t* active, int resample_mode,
+                      const int32_t* chosen, double* log_zetas_out, int32_t* status_out, int32_t* traj_out) {
+    if (!chosen || !traj_out) return fail(EPIPF_EINVAL, "NULL argument");
+    return run_impl(c, n_chains, theta, d, obs_model, probs, keys, filter_index, active, resample_mode, chosen,
+                    log_zetas_out, status_out, traj_out);
+}
+
 int epipf_copy_history(epipf_ctx* c, int n_chains, int32_t* hidden_out, int32_t* ancestry_out) {
     if (!c) return fail(EPIPF_EINVAL, "NULL context");
     if (!c->have_run) return fail(EPIPF_ESTATE, "no filter has run on this context");
@@ -596,7 +683,8 @@ int epipf_path_sample(epipf_ctx* c, int n_chains, const int32_t* chosen, int32_t
     PathArgs a{};
     a.n_chains = n_chains; a.N = c->N; a.T = c->last_T; a.C = c->C;
     a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride;
-    a.hidden = c->hidden; a.ancestry = c->ancestry; a.chosen = c->chosen; a.status = c->status; a.traj = c->traj;
+    a.hidden = c->hidden; a.ancestry = c->ancestry; a.chosen = c->chosen; a.cp = c->cp; a.status = c->status;
+    a.traj = c->traj;
     hipError_t le = launch_path_sample(a, c->stream);
     if (le != hipSuccess) return fail(EPIPF_EHIP, "path kernel launch failed: %s", hipGetErrorString(le));
     HIP_TRY(hipMemcpyAsync(traj_out, c->traj, sizeof(int32_t) * (size_t)n_chains * a.T * a.C, hipMemcpyDeviceToHost, c->stream));

@@ -93,11 +93,15 @@ struct ChainParam {
     uint32_t k0, k1;           // Philox key
     uint32_t f;                // filter index
     uint32_t flags;            // kChainFastSsa: the certified f32 event loop may run (EPIPF_SSA_FAST=0 clears it)
+    int32_t skip;              // 1: this chain runs no filter in this batch (epipf_run's active[] = 0)
+    int32_t chosen;            // epipf_run_sampled: the path sampler's final particle (pmcmc.py:241), -1: none
     float thetaf[kMaxTheta];   // theta rounded to f32 on the host (scalar loads: the fast path's rates stay in SGPRs)
     float clock_slack;         // >= 1: widens the f32 loop's clock band (more replays, same results); tests only
     float band_slack;          // >= 1: widens the channel decision's band (more exact decisions and redone chunks,
                                // same results); tests only
 };
+// chain status codes (include/epipf.h's EPIPF_STATUS_*; epipf_api.cpp checks they agree)
+constexpr int32_t kStatusOk = 0, kStatusDegenerate = 1, kStatusSkipped = 2;
 constexpr uint32_t kChainFastSsa = 1u;   // (all models)
 constexpr uint32_t kChainSeqDecide = 2u; // lane groups: sequential decision pass (EPIPF_GROUP_DECIDE=seq; A/B, tests)
 
@@ -1078,8 +1082,20 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 }
 
 // row: the particle's output row, holding its parent state on entry and its new state on return (every lane reads
-// it; the state is not kept in registers across the replay).
-template <int MODEL, int G>
+// it; the state is not kept in registers across the replay).  WAVE: the caller's workgroup has other waves (the
+// one-workgroup filter), so the row is ordered by a wave-level LDS sync instead of a workgroup barrier.
+template <bool WAVE>
+__device__ __forceinline__ void replay_sync() {
+    if constexpr (WAVE) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else {
+        __syncthreads();
+    }
+}
+
+template <int MODEL, int G, bool WAVE = false>
 __device__ __forceinline__ int coop_replay(int32_t* row, const ChainParam& cp, uint32_t j, uint32_t ptag, double tmax,
                                            const LogTab* __restrict__ tab) {
     using F = FastSsa<MODEL, G>;
@@ -1132,7 +1148,7 @@ __device__ __forceinline__ int coop_replay(int32_t* row, const ChainParam& cp, u
             int32_t v[C];
 #pragma unroll
             for (int c = 0; c < C; ++c) v[c] = (int32_t)readlane_f64(xs[c], stop);
-            __syncthreads();                             // every lane has read the parent row
+            replay_sync<WAVE>();                         // every lane has read the parent row
             if (lane == 0) {
 #pragma unroll
                 for (int c = 0; c < C; ++c) row[c] = v[c];
@@ -1147,7 +1163,7 @@ __device__ __forceinline__ int coop_replay(int32_t* row, const ChainParam& cp, u
 #pragma unroll
     for (int c = 0; c < C; ++c) xf[c] = (double)row[c];
     st.save(xf);
-    __syncthreads();
+    replay_sync<WAVE>();
     if (lane == 0) {
 #pragma unroll
         for (int c = 0; c < C; ++c) row[c] = (int32_t)xf[c];

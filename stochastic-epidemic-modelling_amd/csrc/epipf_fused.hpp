@@ -22,6 +22,9 @@
 //
 // LDS: log table | ChainParam | tau exchange [waves][64] | red[16] | wraw, wloc [B 64] | bsum [B] | bpex [B + 64] |
 //      Y [T K] | log n! [2 (lf_max + 1)] | rows [2][N][C] int32
+// The weights, their in-block prefixes and the block sums are double-buffered by step parity like the rows: with one
+// lane per particle (W = 1) a step has no barrier between a wave's resampling (reading step p - 1's) and its weights
+// (writing step p's), so another wave may still be searching the previous ones.
 #pragma once
 #include "epipf_group.hpp"
 
@@ -30,8 +33,8 @@ namespace epipf {
 constexpr int kCpDoubles = (int)((sizeof(ChainParam) + 15) / 16 * 2);
 inline size_t fused_lds_bytes(int N, int C, int threads, int TK, int lf_n) {
     const int B = (N + 63) / 64;
-    const size_t dbl = 2 * (size_t)kLogTabEntries + kCpDoubles + (size_t)(threads / 64) * 64 + 16 + 2 * (size_t)B * 64 +
-                       B + (B + 64) + (size_t)TK + (size_t)lf_n;
+    const size_t dbl = 2 * (size_t)kLogTabEntries + kCpDoubles + (size_t)(threads / 64) * 64 + 16 + 4 * (size_t)B * 64 +
+                       2 * B + (B + 64) + (size_t)TK + (size_t)lf_n;
     return dbl * sizeof(double) + sizeof(int32_t) * 2 * (size_t)N * C;
 }
 
@@ -53,18 +56,19 @@ __global__ __launch_bounds__(kFusedMaxThreads) void pf_filter_wg_kernel(StepArgs
     ChainParam* cps = reinterpret_cast<ChainParam*>(smem + 2 * kLogTabEntries);   // the chain's parameters
     double* xch = smem + 2 * kLogTabEntries + kCpDoubles;   // group_propagate's tau exchange (exact clock), [nw][64]
     double* red = xch + nw * 64;                         // [0]: the step's total, for every wave
-    double* wraw = red + 16;                             // the last step's weights, [B 64]
-    double* wloc = wraw + B * 64;                        // their in-block inclusive prefix
-    double* bsum = wloc + B * 64;                        // block sums [B]
-    double* bpex = bsum + B;                             // exclusive prefix of the block sums [B] (+ 64 scratch)
+    double* wraw = red + 16;                             // weights by step parity, [2][B 64]
+    double* wloc = wraw + 2 * B * 64;                    // their in-block inclusive prefixes, [2][B 64]
+    double* bsum = wloc + 2 * B * 64;                    // block sums, [2][B]
+    double* bpex = bsum + 2 * B;                         // exclusive prefix of the block sums [B] (+ 64 scratch)
     const int TK = a.fused_y ? T * Sh::K : 0, lf_n = a.fused_lf ? 2 * (a.lf_max + 1) : 0;
     double* ys = bpex + B + 64;                          // Y [T][K] (a.fused_y)
     double* lfs = ys + TK;                               // log n! hi [lf_max + 1], lo [lf_max + 1] (a.fused_lf)
     int32_t* rows = reinterpret_cast<int32_t*>(lfs + lf_n);   // states [2][N][C]: step parity
     const int chain = a.chain0 + (int)blockIdx.x;
     const int tid = (int)threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    if (a.status[chain] != 0) return;                    // skipped (block-uniform)
     const ChainParam cp = a.cp[chain];
+    if (tid == 0) a.status[chain] = cp.skip ? kStatusSkipped : kStatusOk;   // this run's chain status
+    if (cp.skip) return;                                 // block-uniform
     for (int i = tid; i < kLogTabEntries; i += nthr) tab[i] = a.logtab[i];
     {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(a.cp + chain);
@@ -109,7 +113,7 @@ __global__ __launch_bounds__(kFusedMaxThreads) void pf_filter_wg_kernel(StepArgs
     double lzp = 0.0;                                    // log_zeta[p - 1] (thread 0)
     if (tid == 0) lz[0] = 0.0;
     unsigned long long events = 0;
-    const int gl = tid & (W - 1), pl = tid / W;          // SSA: group of W lanes per particle pl
+    const int gl = tid & (W - 1), pl = tid / W;          // SSA (W > 1): group of W lanes per particle pl
     __syncthreads();
 #ifdef EPIPF_PHASE_TIMING
     unsigned long long fph[6] = {0, 0, 0, 0, 0, 0}, fm0 = __builtin_readcyclecounter(), fm1;
@@ -122,9 +126,15 @@ __global__ __launch_bounds__(kFusedMaxThreads) void pf_filter_wg_kernel(StepArgs
         const int cur = p & 1, prev = cur ^ 1;
         int32_t* rprev = rows + (size_t)prev * N * C;
         int32_t* rcur = rows + (size_t)cur * N * C;
+        double* wr_prev = wraw + prev * B * 64;         // the weights step p resamples from ...
+        double* wl_prev = wloc + prev * B * 64;
+        double* bs_prev = bsum + prev * B;
+        double* wr_cur = wraw + cur * B * 64;           // ... and the ones it produces for step p + 1
+        double* wl_cur = wloc + cur * B * 64;
+        double* bs_cur = bsum + cur * B;
         // (b) likelihood, pmcmc.py:183: the block-sum prefix (the step kernels' scan_block_sums<64>, S = 1)
         if (wave == 0) {
-            const double total = scan_block_sums<64, true>(bsum, B, bpex, bsum, red + 1);
+            const double total = scan_block_sums<64, true>(bs_prev, B, bpex, bs_prev, red + 1);
             if (lane == 0) red[0] = total;
         }
         __syncthreads();
@@ -141,8 +151,8 @@ __global__ __launch_bounds__(kFusedMaxThreads) void pf_filter_wg_kernel(StepArgs
             lzp = lzp + log(total / (double)N);
             lz[p] = lzp;
         }
-        // (d) multinomial (or systematic) draw, certified search, exact fallback; gather (:188-199)
-        if (pt) {
+        // (d) multinomial (or systematic) draw, certified search, exact fallback (:188-193); lanes of the particle phase
+        auto draw_ancestor = [&]() __attribute__((always_inline)) -> int {
             double U = 0.0;
             int anc = 0;
             bool certified = true, ambiguous = false;
@@ -156,55 +166,26 @@ __global__ __launch_bounds__(kFusedMaxThreads) void pf_filter_wg_kernel(StepArgs
                     U = ((double)j + u01(r.x, r.y)) / (double)N;
                 }
                 // the flat in-block search (two rounds of 7 independent LDS loads instead of 6 dependent ones)
-                anc = resample_search<64, true>(U, bpex, bsum, B, total, wloc, N, a.cert_k, certified, a.ref_k,
+                anc = resample_search<64, true>(U, bpex, bs_prev, B, total, wl_prev, N, a.cert_k, certified, a.ref_k,
                                                 ambiguous);
             }
             if (ambiguous) atomicAdd(counter_slot(a.counters) + 6, 1ull);
             if (__any(!certified)) {                     // wave-uniform
-                const int e = resample_exact_wave(!certified, U, wraw, N);
+                const int e = resample_exact_wave(!certified, U, wr_prev, N);
                 if (!certified) {
                     anc = e;
                     atomicAdd(counter_slot(a.counters) + 1, 1ull);
                 }
             }
-            if (j < N) {
-                anc = checked_index(anc, N);
-                ancg[(size_t)p * N + j] = anc;
-#pragma unroll
-                for (int c = 0; c < C; ++c) rcur[j * C + c] = rprev[anc * C + c];
-            }
-        }
-        __syncthreads();
-        EPIPF_FUSED_MARK(1);
-        // (g) propagate over [0, 1]: W lanes per particle
-        double x[C];
-        int nev = 0;
-        if (pl < N) {                                    // group-uniform
-            double x0[C];
-#pragma unroll
-            for (int c = 0; c < C; ++c) x0[c] = (double)rcur[pl * C + c];
-            const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
-            nev = group_propagate<MODEL, G, W, 1, NoDays, true>(x0, x, cp, (uint32_t)pl, ptag, 1.0, tab, xch + wave * 64);
-            if (nev < 0)                                 // a clock decision within the certified bound (rare)
-                nev = group_propagate<MODEL, G, W, 1, NoDays, false>(x0, x, cp, (uint32_t)pl, ptag, 1.0, tab,
-                                                                     xch + wave * 64);
-        }
-        __syncthreads();                                 // every group has read its parent row
-        EPIPF_FUSED_MARK(2);
-        if (pl < N && gl == 0) {
-#pragma unroll
-            for (int c = 0; c < C; ++c) rcur[pl * C + c] = (int32_t)x[c];
-            events += (unsigned long long)nev;
-        }
-        __syncthreads();
-        EPIPF_FUSED_MARK(3);
-        // store, weights for step p + 1, in-block scans (:178-181, :222-231)
-        if (pt) {
+            anc = checked_index(anc, N);
+            if (j < N) ancg[(size_t)p * N + j] = anc;
+            return anc;
+        };
+        // store, weights for step p + 1, in-block scans (:178-181, :222-231): lane j of the particle phase, its state
+        // in xs (read by the scan's other lanes only through wraw / wloc / bsum)
+        auto weigh = [&](const double* xs) __attribute__((always_inline)) {
             double w = 0.0;
             if (j < N) {
-                double xs[C];
-#pragma unroll
-                for (int c = 0; c < C; ++c) xs[c] = (double)rcur[j * C + c];
                 int32_t* hc = hist + ((size_t)p * N + j) * C;
 #pragma unroll
                 for (int c = 0; c < C; ++c) hc[c] = (int32_t)xs[c];
@@ -213,13 +194,104 @@ __global__ __launch_bounds__(kFusedMaxThreads) void pf_filter_wg_kernel(StepArgs
             }
             if (p + 1 < T) {
                 const double loc = block_inclusive_scan<64>(w, nullptr);
-                wraw[j] = w;
-                wloc[j] = loc;
-                if (lane == 63) bsum[wave] = loc;
+                wr_cur[j] = w;
+                wl_cur[j] = loc;
+                if (lane == 63) bs_cur[wave] = loc;
             }
+        };
+        const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
+        if constexpr (W == 1) {
+            // one lane per particle (pf_step_kernel's SSA): draw, gather, propagate, store and weigh on the same lane --
+            // no barrier inside the step.  Lanes the certified f32 loop hands back run the exact loop (ineligible) or
+            // are replayed by their whole wave (coop_replay) on their LDS row.
+            double x[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) x[c] = 0.0;
+            int nev = 0, iters = 0;
+            bool fast_ok = false, eligible = false;
+            const int anc = draw_ancestor();
+            if (j < N) {
+#pragma unroll
+                for (int c = 0; c < C; ++c) x[c] = (double)rprev[anc * C + c];
+                fast_ok = fast_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, nev, iters, eligible);
+            }
+            const bool exact = j < N && !fast_ok;
+            if (__any(exact)) {                          // wave-uniform
+                if (exact && !eligible) {
+                    int ex_iters = 0;
+                    nev = exact_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, tab, ex_iters);
+                }
+                unsigned long long pend = __ballot(exact && eligible);
+                if (pend) {
+                    if (j < N) {
+#pragma unroll
+                        for (int c = 0; c < C; ++c) rcur[j * C + c] = (int32_t)x[c];   // replayed lanes: the parent
+                    }
+                    lds_sync<true>();
+                    while (pend) {
+                        const int L = (int)__builtin_ctzll(pend);
+                        pend &= pend - 1ull;
+                        const uint32_t jl = __builtin_amdgcn_readlane((uint32_t)j, L);
+                        const int n = coop_replay<MODEL, G, true>(rcur + (size_t)jl * C, cp, jl, ptag, 1.0, tab);
+                        if (lane == L) nev = n;
+                    }
+                    lds_sync<true>();
+                    if (j < N) {
+#pragma unroll
+                        for (int c = 0; c < C; ++c) x[c] = (double)rcur[j * C + c];
+                    }
+                }
+            }
+            if (j < N) {
+#pragma unroll
+                for (int c = 0; c < C; ++c) rcur[j * C + c] = (int32_t)x[c];
+                events += (unsigned long long)nev;
+            }
+            EPIPF_FUSED_MARK(2);
+            weigh(x);
+            __syncthreads();                             // this step's states and weights before the next step
+            EPIPF_FUSED_MARK(4);
+        } else {
+            // gather (:195-199) into this step's rows, then W lanes per particle
+            if (pt) {
+                const int anc = draw_ancestor();
+                if (j < N) {
+#pragma unroll
+                    for (int c = 0; c < C; ++c) rcur[j * C + c] = rprev[anc * C + c];
+                }
+            }
+            __syncthreads();
+            EPIPF_FUSED_MARK(1);
+            double x[C];
+            int nev = 0;
+            if (pl < N) {                                // group-uniform
+                double x0[C];
+#pragma unroll
+                for (int c = 0; c < C; ++c) x0[c] = (double)rcur[pl * C + c];
+                nev = group_propagate<MODEL, G, W, 1, NoDays, true>(x0, x, cp, (uint32_t)pl, ptag, 1.0, tab,
+                                                                    xch + wave * 64);
+                if (nev < 0)                             // a clock decision within the certified bound (rare)
+                    nev = group_propagate<MODEL, G, W, 1, NoDays, false>(x0, x, cp, (uint32_t)pl, ptag, 1.0, tab,
+                                                                         xch + wave * 64);
+            }
+            __syncthreads();                             // every group has read its parent row
+            EPIPF_FUSED_MARK(2);
+            if (pl < N && gl == 0) {
+#pragma unroll
+                for (int c = 0; c < C; ++c) rcur[pl * C + c] = (int32_t)x[c];
+                events += (unsigned long long)nev;
+            }
+            __syncthreads();
+            EPIPF_FUSED_MARK(3);
+            if (pt) {
+                double xs[C];
+#pragma unroll
+                for (int c = 0; c < C; ++c) xs[c] = j < N ? (double)rcur[j * C + c] : 0.0;
+                weigh(xs);
+            }
+            __syncthreads();
+            EPIPF_FUSED_MARK(4);
         }
-        __syncthreads();
-        EPIPF_FUSED_MARK(4);
     }
 #ifdef EPIPF_PHASE_TIMING
     if (tid == 0 && blockIdx.x == 0)
@@ -233,7 +305,7 @@ __global__ __launch_bounds__(kFusedMaxThreads) void pf_filter_wg_kernel(StepArgs
     }
 }
 
-// launch table: W lanes per particle (2, 4, 8, 16), one workgroup of fused_threads(N, W) threads per chain
+// launch table: W lanes per particle (1, 2, 4, 8, 16), one workgroup of fused_threads(N, W) threads per chain
 template <int MODEL, int G, int OBS, int W>
 static void launch_fused_t(const StepArgs& a, int n_chains, int threads, size_t lds, hipStream_t s) {
     hipLaunchKernelGGL((pf_filter_wg_kernel<MODEL, G, OBS, W>), dim3(n_chains), dim3(threads), lds, s, a);
@@ -242,6 +314,7 @@ static void launch_fused_t(const StepArgs& a, int n_chains, int threads, size_t 
 template <int MODEL, int G, int OBS>
 static FusedFn pick_fused_w(int W) {
     switch (W) {
+        case 1: return launch_fused_t<MODEL, G, OBS, 1>;
         case 2: return launch_fused_t<MODEL, G, OBS, 2>;
         case 4: return launch_fused_t<MODEL, G, OBS, 4>;
         case 8: return launch_fused_t<MODEL, G, OBS, 8>;

@@ -74,7 +74,8 @@ struct PathArgs {
     size_t hist_stride, anc_stride;
     const int32_t* hidden;
     const int32_t* ancestry;
-    const int32_t* chosen;
+    const int32_t* chosen;      // per chain, or null: ChainParam::chosen (epipf_run_sampled)
+    const ChainParam* cp;
     const int32_t* status;      // the last run's chain status: only EPIPF_STATUS_OK chains are walked
     int32_t* traj;
 };

@@ -36,8 +36,10 @@ __global__ __launch_bounds__(WG) void pf_init_kernel(StepArgs a) {
     // a.wg hold no particle and weigh 0 in the scan)
     const bool mine = (int)threadIdx.x < a.wg;
     const int j = bp.b * a.wg + (int)threadIdx.x;
-    if (a.status[chain] != 0) return;
     const ChainParam cp = a.cp[chain];
+    // the chain's status for this run: skipped or running (the step kernels read it; a degenerate step sets 1)
+    if (bp.b == 0 && threadIdx.x == 0) a.status[chain] = cp.skip ? kStatusSkipped : kStatusOk;
+    if (cp.skip) return;
     double x[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) x[c] = 0.0;
@@ -224,7 +226,12 @@ __global__ void path_sample_kernel(PathArgs a) {
         for (int i = 0; i < a.T * a.C; ++i) out[i] = 0;   // stale or unwritten, so it is not walked (zeros returned)
         return;
     }
-    int chosen = checked_index(a.chosen[chain], a.N);
+    const int pick = a.chosen ? a.chosen[chain] : a.cp[chain].chosen;   // epipf_path_sample / epipf_run_sampled
+    if (pick < 0) {                                  // no path asked of this chain
+        for (int i = 0; i < a.T * a.C; ++i) out[i] = 0;
+        return;
+    }
+    int chosen = checked_index(pick, a.N);
     const int32_t* hid = a.hidden + (size_t)chain * a.hist_stride;
     const int32_t* anc = a.ancestry + (size_t)chain * a.anc_stride;
     for (int c = 0; c < a.C; ++c) out[(size_t)(a.T - 1) * a.C + c] = hid[((size_t)(a.T - 1) * a.N + chosen) * a.C + c];

@@ -116,8 +116,10 @@ class Engine:
         self._pop = key
 
     # ------------------------------------------------------------------ the filter
-    def run(self, thetas, probs, keys, filter_indices, observations=False, active=None, resample="multinomial"):
-        """Run len(thetas) independent filters.  Returns (log_zetas [n, T], status [n])."""
+    def run(self, thetas, probs, keys, filter_indices, observations=False, active=None, resample="multinomial",
+            chosen=None):
+        """Run len(thetas) independent filters.  Returns (log_zetas [n, T], status [n]); with chosen [n] (the path
+        sampler's final particles, -1 for none) also the sampled trajectories [n, T, C] int32 (epipf_run_sampled)."""
         thetas = np.ascontiguousarray(np.asarray(thetas, dtype=np.float64))
         n = thetas.shape[0]
         probs = np.ascontiguousarray(np.broadcast_to(np.asarray(probs, dtype=np.float64), (n,)))
@@ -128,12 +130,21 @@ class Engine:
         lz = np.empty((n, self.T), dtype=np.float64)
         st = np.empty(n, dtype=np.int32)
         mode = _lib.RESAMPLE_MULTINOMIAL if resample == "multinomial" else _lib.RESAMPLE_SYSTEMATIC
-        check(self._L.epipf_run(self._h, n, ptr(thetas), thetas.shape[1],
-                                _lib.OBS_NORMAL if observations else _lib.OBS_BINOMIAL, ptr(probs), ptr(keys),
-                                ptr(fidx), ptr(act), mode, ptr(lz), ptr(st)), "epipf_run")
+        obs = _lib.OBS_NORMAL if observations else _lib.OBS_BINOMIAL
+        if chosen is None:
+            check(self._L.epipf_run(self._h, n, ptr(thetas), thetas.shape[1], obs, ptr(probs), ptr(keys), ptr(fidx),
+                                    ptr(act), mode, ptr(lz), ptr(st)), "epipf_run")
+        else:
+            ch = np.ascontiguousarray(np.asarray(chosen, dtype=np.int32).reshape(-1))
+            if ch.size != n:
+                raise ValueError(f"chosen has {ch.size} entries for {n} filters")
+            tr = np.empty((n, self.T, self.C), dtype=np.int32)
+            check(self._L.epipf_run_sampled(self._h, n, ptr(thetas), thetas.shape[1], obs, ptr(probs), ptr(keys),
+                                            ptr(fidx), ptr(act), mode, ptr(ch), ptr(lz), ptr(st), ptr(tr)),
+                  "epipf_run_sampled")
         self._last_n = n
         _PARTICLE_STEPS[0] += (n if act is None else int(np.count_nonzero(act))) * self.N * self.T
-        return lz, st
+        return (lz, st) if chosen is None else (lz, st, tr)
 
     def history(self, n_chains=None):
         """(hidden [n, T, N, C] int32, ancestry [n, T, N] int32) of the last run."""

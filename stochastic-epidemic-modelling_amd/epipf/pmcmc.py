@@ -17,6 +17,7 @@ Random numbers.  The reference draws everything from numpy's global MT19937.  He
 Under np.random.seed(s) + seed_stream(k) the results equal the reference's driven by the same
 keyed stream (tests/golden/make_golden.py), which is how parity is tested.
 """
+import ctypes
 import math
 from enum import Enum
 
@@ -187,6 +188,39 @@ def legacy_randint(rng, n, bg=None):
             return int(v)
 
 
+class _MTPeek:
+    """The value the next legacy_randint(rng, n) will return, read off the MT19937 state without consuming it (numpy's
+    mt19937_state: uint32 key[624], int pos; a draw tempers key[pos++]), or None when the draw would have to regenerate
+    the state first.  Lets the path sampler's final particle (pmcmc.py:241), drawn by the reference after the filter,
+    be handed to the device with the filter itself (epipf_run_sampled); the real draw still happens in its place and
+    is checked against the peeked one."""
+
+    __slots__ = ("_bg", "_key", "_pos")
+
+    def __init__(self, bg):
+        addr = bg.ctypes.state_address
+        self._bg = bg                                          # keeps the state alive
+        self._key = (ctypes.c_uint32 * 624).from_address(addr)
+        self._pos = ctypes.c_int.from_address(addr + 624 * 4)
+
+    def randint(self, n):
+        r = int(n) - 1
+        if r <= 0:
+            return 0
+        mask = (1 << r.bit_length()) - 1
+        pos, key = self._pos.value, self._key
+        while pos < 624:
+            y = key[pos]
+            pos += 1
+            y ^= y >> 11
+            y ^= (y << 7) & 0x9D2C5680
+            y ^= (y << 15) & 0xEFC60000
+            y ^= y >> 18
+            if y & mask <= r:
+                return y & mask
+        return None
+
+
 def _log_ratio(lz_new, lz_old):
     """Underflow-free MH acceptance probability min(1, z'/z) from log-likelihoods (the symmetric
     Gaussian proposal terms of pmcmc.py:380-391 cancel)."""
@@ -217,6 +251,8 @@ class ChainSampler:
     or [chains, d, d].
     rngs: per-chain RandomState-like objects (proposals, path picks, acceptance uniforms).
     keys: per-chain Philox keys for the filters; filter indices count from `filter_index_start`."""
+
+    FUSE_PATH_CHAINS = 16
 
     def __init__(self, Y, type_model, parameters, h, adaptive=False, sigma=None, iters=1000, observations=False,
                  probs=.1, n_particles=1000, n_population=4820, mu=20, *, rngs, keys, device=0,
@@ -277,6 +313,11 @@ class ChainSampler:
         self._uniform = [r.random_sample for r in self.rngs]
         self._raw = [_raw_words(r) for r in self.rngs]
         self._dbuf = np.empty((nc, d))
+        # up to FUSE_PATH_CHAINS chains the path sampler rides on the filter's launch (epipf_run_sampled): its
+        # randint is peeked before the filter (_MTPeek); more chains amortise the separate call better than the peeks
+        self._peek = None
+        if nc <= self.FUSE_PATH_CHAINS and all(b is not None for b in self._raw):
+            self._peek = [_MTPeek(b) for b in self._raw]
         self.acceptances = [1] * nc
         self.dth = d - (1 if probs is None else 0)
         self.i = 0
@@ -401,13 +442,32 @@ class ChainSampler:
                 self.fnext[c] += 1
                 self.filters_run[c] += 1
             self._bind()
-            lz, st = self.eng.run(np.ascontiguousarray(th_all), pr_all, self.keys, fidx,
-                                  observations=self.observations, active=live.astype(np.int32), resample=self.resample)
+            pre = None
+            if self._peek is not None:                            # the path pick, peeked (see _MTPeek)
+                pre = np.full(nc, -1, dtype=np.int32)
+                for c in lv.tolist():
+                    v = self._peek[c].randint(self.N)
+                    if v is None:
+                        pre = None
+                        break
+                    pre[c] = v
+            out = self.eng.run(np.ascontiguousarray(th_all), pr_all, self.keys, fidx, observations=self.observations,
+                               active=live.astype(np.int32), resample=self.resample, chosen=pre)
+            lz, st = out[0], out[1]
             self.last_active = int(lv.size)
             ok = np.flatnonzero(live & (st == _lib.STATUS_OK))    # degenerate filters: rejected, :365-369
             if ok.size:
                 okl = ok.tolist()
-                tr = self._path_sample(okl)
+                if pre is None:
+                    tr = self._path_sample(okl)
+                else:                                             # the reference's randint, drawn in its place
+                    tr = out[2]
+                    real = [legacy_randint(self.rngs[c], self.N, self._raw[c]) for c in okl]
+                    if real != pre[ok].tolist():                  # (never seen) walk the drawn picks instead
+                        self._peek = None
+                        chosen = np.zeros(nc, dtype=np.int32)
+                        chosen[ok] = real
+                        tr = self.eng.path_sample(chosen)
                 lzT = lz[:, -1]
                 take = []
                 uniform = self._uniform

@@ -24,7 +24,7 @@ class OracleEngine:
     def set_population(self, npop, mu):
         self.npop, self.mu = np.atleast_1d(npop), np.atleast_1d(mu)
 
-    def run(self, thetas, probs, keys, fidx, observations=False, active=None, resample="multinomial"):
+    def run(self, thetas, probs, keys, fidx, observations=False, active=None, resample="multinomial", chosen=None):
         n = len(thetas)
         probs = np.broadcast_to(probs, (n,))
         keys = np.broadcast_to(np.asarray(keys, dtype=np.uint64), (n,))
@@ -46,18 +46,29 @@ class OracleEngine:
             st[c] = o["status"]
             lz[c] = o["log_zetas"]
             self.hist[c] = (o["hidden"], o["ancestry"])
-        return lz, st
+        if chosen is None:
+            return lz, st
+        # epipf_run_sampled: the path sampler on the picks handed over with the filter (zeros: -1 or not OK)
+        tr = np.zeros((n, self.T, self.C), dtype=np.int32)
+        for c in range(n):
+            if st[c] == 0 and chosen[c] >= 0:
+                tr[c] = self._walk(c, int(chosen[c]))
+        return lz, st, tr
+
+    def _walk(self, c, ch):
+        hid, anc = self.hist[c]
+        out = np.zeros((self.T, self.C), dtype=np.int32)
+        out[-1] = hid[-1, ch]
+        for p in range(self.T - 2, -1, -1):
+            ch = anc[p, ch]
+            out[p] = hid[p, ch]
+        return out
 
     def path_sample(self, chosen):
         out = np.zeros((len(chosen), self.T, self.C), dtype=np.int32)
         for c, ch in enumerate(chosen):
-            if c not in self.hist:
-                continue
-            hid, anc = self.hist[c]
-            out[c, -1] = hid[-1, ch]
-            for p in range(self.T - 2, -1, -1):
-                ch = anc[p, ch]
-                out[c, p] = hid[p, ch]
+            if c in self.hist:
+                out[c] = self._walk(c, int(ch))
         return out
 
 

@@ -11,6 +11,13 @@ import oracle
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _fused_on(monkeypatch):
+    """The one-workgroup filter wherever it is eligible (EPIPF_FUSED=1; the default measures both paths first)."""
+    monkeypatch.setenv("EPIPF_FUSED", "1")
+
+
 MODELS = ["sir", "sir_normal", "seir", "sir_subgroups", "sir_subgroups2"]
 
 
@@ -60,19 +67,25 @@ def _run_both(monkeypatch, *args, **kw):
     try:
         b = _run(*args, **kw)
     finally:
-        monkeypatch.delenv("EPIPF_FUSED")
+        monkeypatch.setenv("EPIPF_FUSED", "1")
     return a, b
 
 
+@pytest.mark.parametrize("lanes", [0, 1, 2, 4, 16])
 @pytest.mark.parametrize("N", [1, 37, 64, 100, 129, 200, 256])
 @pytest.mark.parametrize("model", MODELS)
-def test_fused_filter_matches_oracle(datasets_golden, model, N):
+def test_fused_filter_matches_oracle(datasets_golden, monkeypatch, model, N, lanes):
+    """Every SSA width of the one-workgroup filter (EPIPF_FUSED_LANES, read at create; 0: the automatic one)."""
+    if N * lanes > 512:
+        pytest.skip("N W lanes exceed one workgroup")
+    monkeypatch.setenv("EPIPF_FUSED_LANES", str(lanes))
     c = _case(datasets_golden, model)
     name = c.get("model", model)
     keys, fidx = [71, 72], [3, 8]
     lz, st, hid, anc, s = _run(name, c, N, 2, keys, fidx)
     assert s["last_fused"] == 1
-    assert s["last_lanes"] == next(W for W in (16, 8, 4, 2) if N * W <= 512 or W == 2)
+    if lanes:
+        assert s["last_lanes"] == lanes
     for ch in range(2):
         o = oracle.particle_filter(c["Y"], name, c["theta"], c["obs"], c["probs"], N, c["npop"], c["mu"],
                                    key=keys[ch], filter_index=fidx[ch])
@@ -100,7 +113,7 @@ def test_fused_threshold_and_explicit_lanes(datasets_golden, monkeypatch):
         assert eng.stats()["last_fused"] == want, (N, lanes, env)
         eng.close()
         if env is not None:
-            monkeypatch.delenv("EPIPF_FUSED")
+            monkeypatch.setenv("EPIPF_FUSED", "1")
 
 
 @pytest.mark.parametrize("model", MODELS)
@@ -203,5 +216,63 @@ def test_fused_counts_the_same_events(datasets_golden, monkeypatch):
         eng.run(np.tile([2.0, 1.0], (4, 1)), [0.1] * 4, [1, 2, 3, 4], [0] * 4)
         ev.append(eng.stats()["events"])
         eng.close()
-    monkeypatch.delenv("EPIPF_FUSED")
+    monkeypatch.setenv("EPIPF_FUSED", "1")
     assert ev[0] == ev[1] > 0
+
+
+@pytest.mark.parametrize("N", [100, 700])
+def test_run_sampled_equals_run_then_path_sample(datasets_golden, N):
+    """epipf_run_sampled (the path sampler on the filter's stream, picks handed over with the filter) against
+    epipf_run + epipf_path_sample, on the one-workgroup filter (N = 100) and the step launches (N = 700): the same
+    likelihoods and statuses, the same paths, zeros for a skipped chain, a chain with pick -1 and a degenerate one."""
+    from epipf.engine import Engine
+    c = _case(datasets_golden, "sir")
+    Y = c["Y"]
+    for degenerate in (False, True):
+        if degenerate:
+            Y = Y.copy()
+            Y[5:] = 1e7
+        eng = Engine("sir", 1, N, Y.shape[0], 4)
+        eng.set_observations(Y)
+        eng.set_population(c["npop"], c["mu"])
+        th = np.tile([2.0, 1.0], (4, 1))
+        act = np.array([1, 1, 0, 1], dtype=np.int32)
+        keys, fidx = [3, 4, 5, 6], [9, 9, 9, 9]
+        chosen = np.array([5, -1, 7, N - 1], dtype=np.int32)
+        lz, st = eng.run(th, [0.1] * 4, keys, fidx, active=act)
+        ref = eng.path_sample(np.maximum(chosen, 0))
+        lz2, st2, tr = eng.run(th, [0.1] * 4, keys, fidx, active=act, chosen=chosen)
+        eng.close()
+        np.testing.assert_array_equal(st, st2)
+        np.testing.assert_array_equal(lz, lz2)
+        assert int(st[2]) == 2
+        for ch in range(4):
+            if st[ch] == 0 and chosen[ch] >= 0:
+                np.testing.assert_array_equal(tr[ch], ref[ch])
+            else:
+                assert not tr[ch].any()
+        if degenerate:
+            assert (st[[0, 1, 3]] == 1).all()
+
+
+def test_automatic_choice_times_both_paths_with_identical_results(datasets_golden, monkeypatch):
+    """EPIPF_FUSED=auto (the default): a batch size's first six runs alternate the one-workgroup filter and the step
+    launches (fused first), then one path stays; every run's outputs are the same."""
+    from epipf.engine import Engine
+    monkeypatch.setenv("EPIPF_FUSED", "auto")
+    c = _case(datasets_golden, "seir")
+    eng = Engine("seir", 1, 90, c["Y"].shape[0], 3)
+    eng.set_observations(c["Y"])
+    eng.set_population(c["npop"], c["mu"])
+    th = np.tile([4.0, 1.0, 1.0], (3, 1))
+    used, outs = [], []
+    for r in range(9):
+        lz, st = eng.run(th, [0.1] * 3, [1, 2, 3], [5, 5, 5])
+        used.append(eng.stats()["last_fused"])
+        outs.append((lz.copy(), st.copy(), *eng.history(3)))
+    eng.close()
+    assert used[:6] == [1, 0, 1, 0, 1, 0]
+    assert len(set(used[6:])) == 1
+    for o in outs[1:]:
+        for x, y in zip(o, outs[0]):
+            np.testing.assert_array_equal(x, y)

@@ -1,0 +1,66 @@
+"""Host RNG shortcuts of the MH loop against numpy itself (CPU): legacy_randint draws what RandomState.randint(0, n)
+draws and leaves the stream where it leaves it; _MTPeek reads that value off the MT19937 state without consuming it;
+the per-chain proposal arithmetic equals mvn_apply's."""
+import numpy as np
+import pytest
+
+from epipf.pmcmc import _MTPeek, _raw_words, legacy_randint, mvn_apply, mvn_factor
+
+
+def test_legacy_randint_equals_randint_and_its_consumption():
+    rs = np.random.RandomState(5)
+    for t in range(3000):
+        n = int(rs.randint(1, 2**31)) if t % 3 else int(rs.randint(1, 3000))
+        a, b = np.random.RandomState(t), np.random.RandomState(t)
+        for _ in range(3):
+            assert a.randint(0, n) == legacy_randint(b, n)
+        assert a.random_sample() == b.random_sample()
+
+
+def test_legacy_randint_on_the_global_generator_and_fallback():
+    np.random.seed(11)
+    want = [np.random.randint(0, 977) for _ in range(50)]
+    np.random.seed(11)
+    assert [legacy_randint(np.random, 977) for _ in range(50)] == want
+    g = np.random.default_rng(3)                       # not a legacy RandomState: falls back to its own randint-alike
+
+    class R:
+        def randint(self, lo, hi):
+            return int(g.integers(lo, hi))
+    assert _raw_words(R()) is None
+    assert 0 <= legacy_randint(R(), 10) < 10
+
+
+def test_peek_equals_the_next_draw_without_consuming():
+    rs = np.random.RandomState(3)
+    unpeekable = 0
+    for t in range(4000):
+        r = np.random.RandomState(t)
+        r.random_sample(int(rs.randint(0, 700)))      # every position in the 624-word state, regenerations included
+        n = int(rs.randint(1, 2**31)) if t % 2 else int(rs.randint(1, 20000))
+        pk = _MTPeek(_raw_words(r))
+        v = pk.randint(n)
+        again = pk.randint(n)                          # nothing consumed
+        w = legacy_randint(r, n)
+        if v is None:
+            unpeekable += 1
+            assert again is None
+        else:
+            assert v == again == w
+    assert unpeekable < 100                            # only draws that would regenerate the state first
+
+
+@pytest.mark.parametrize("d", [2, 3, 5])
+def test_proposal_into_a_buffer_equals_mvn_apply(d):
+    """ChainSampler.step's np.dot(z, factor, out=row) followed by + theta for all chains == mvn_apply per chain."""
+    rs = np.random.RandomState(d)
+    A = rs.standard_normal((d, d))
+    fac = mvn_factor(0.3 * (A @ A.T))
+    Z = rs.standard_normal((64, d))
+    M = rs.standard_normal((64, d))
+    D = np.empty((64, d))
+    for c in range(64):
+        np.dot(Z[c].reshape(1, d), fac, out=D[c:c + 1])
+    P = D + M
+    for c in range(64):
+        np.testing.assert_array_equal(P[c], mvn_apply(Z[c].copy(), fac, M[c]))
