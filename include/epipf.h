@@ -215,6 +215,21 @@ int epipf_set_lanes(epipf_ctx* ctx, int lanes, int events_per_lane);
 int epipf_get_stats(epipf_ctx* ctx, epipf_stats* out);
 int epipf_reset_stats(epipf_ctx* ctx);
 
+/* Host side of a many-chain MH iteration (epipf.pmcmc.ChainSampler, pmcmc.py:325-406 per chain), in C: each chain's
+ * numpy legacy RandomState draws made on its MT19937 state in place (mt_states[c]: the bit generator's
+ * ctypes.state_address, numpy's mt19937_state), bit-identical to numpy's own and in the reference's order.  No device
+ * work; status codes as the rest of the ABI.
+ * epipf_mh_propose: props_out[c] = multivariate_normal(means[c], .) of pmcmc.py:330 = standard_normal(d) (even d, empty
+ *   gaussian cache) times factors[c] ([d][d], mvn_factor) by dgemv (numpy's own cblas_dgemv, a function pointer:
+ *   the product numpy computes for np.dot) plus means[c].
+ * epipf_mh_decide: for the n chains listed in chains[] (their filters succeeded), in order: chosen_out[c] =
+ *   randint(0, n_particles) (the path sampler's pick, pmcmc.py:241), then accept_out[c] = random_sample() <
+ *   min(1, exp(min(lz_new[c] - lz_old[c], 0))) (the log-space acceptance, 0 for NaN). */
+int epipf_mh_propose(int n_chains, int d, void* const* mt_states, const double* factors, const double* means,
+                     double* props_out, void* dgemv);
+int epipf_mh_decide(int n, const int32_t* chains, void* const* mt_states, int n_particles, const double* lz_new,
+                    const double* lz_old, int32_t* chosen_out, int32_t* accept_out);
+
 const char* epipf_last_error(void);
 int epipf_abi_version(void);
 /* Hash of the library's sources and build flags (16 hex digits; "...-debug" for libepipf_debug.so).  Profiles taken

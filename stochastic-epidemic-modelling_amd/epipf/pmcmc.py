@@ -221,6 +221,43 @@ class _MTPeek:
         return None
 
 
+class _NumpyDgemv:
+    """numpy's own cblas_dgemv (its bundled OpenBLAS), the routine behind np.dot of a (1, d) row and a (d, d) matrix:
+    passed to epipf_mh_propose so that the C proposals round exactly as multivariate_normal's np.dot.  Found once per
+    process and accepted only if it reproduces np.dot bit for bit on random factors; else None (the Python path)."""
+    _ptr = 0
+
+    @classmethod
+    def pointer(cls):
+        if cls._ptr == 0:
+            cls._ptr = None
+            try:
+                import glob
+                import os
+                libdir = os.path.join(os.path.dirname(os.path.dirname(np.__file__)), "numpy.libs")
+                for path in sorted(glob.glob(os.path.join(libdir, "libscipy_openblas64_*.so"))):
+                    f = ctypes.CDLL(path).scipy_cblas_dgemv64_
+                    i64, P = ctypes.c_int64, ctypes.c_void_p
+                    f.argtypes = [ctypes.c_int, ctypes.c_int, i64, i64, ctypes.c_double, P, i64, P, i64,
+                                  ctypes.c_double, P, i64]
+                    rs = np.random.RandomState(12345)
+                    ok = True
+                    for d in (2, 4, 6, 8):
+                        for _ in range(25):
+                            A = rs.standard_normal((d, d))
+                            fac = np.ascontiguousarray(mvn_factor(A @ A.T))
+                            z = rs.standard_normal(d)
+                            y = np.empty(d)
+                            f(101, 112, d, d, 1.0, fac.ctypes.data, d, z.ctypes.data, 1, 0.0, y.ctypes.data, 1)
+                            ok = ok and bool((y == np.dot(z.reshape(1, d), fac).reshape(d)).all())
+                    if ok:
+                        cls._ptr = ctypes.cast(f, ctypes.c_void_p).value
+                        break
+            except (OSError, AttributeError):
+                cls._ptr = None
+        return cls._ptr
+
+
 def _log_ratio(lz_new, lz_old):
     """Underflow-free MH acceptance probability min(1, z'/z) from log-likelihoods (the symmetric
     Gaussian proposal terms of pmcmc.py:380-391 cancel)."""
@@ -256,7 +293,8 @@ class ChainSampler:
 
     def __init__(self, Y, type_model, parameters, h, adaptive=False, sigma=None, iters=1000, observations=False,
                  probs=.1, n_particles=1000, n_population=4820, mu=20, *, rngs, keys, device=0,
-                 mh_ratio="reference", resample="multinomial", filter_index_start=0, engine_chains=0, engine=None):
+                 mh_ratio="reference", resample="multinomial", filter_index_start=0, engine_chains=0, engine=None,
+                 host_draws=True):
         self.rngs = list(rngs)
         self.keys = np.asarray(keys, dtype=np.uint64)
         nc = self.nc = len(self.rngs)
@@ -306,8 +344,9 @@ class ChainSampler:
             raise ValueError(f"sigma must be [{d}, {d}] or [chains, {d}, {d}]")
         self.std = [np.eye(d) if S is None else (S[c] if S.ndim == 3 else S).copy() for c in range(nc)]
         self._fac = [None] * nc                                  # multivariate_normal factor of h * std[c]
-        self.fnext = [int(filter_index_start)] * nc
-        self.filters_run = [0] * nc
+        # per-chain counters as int64 arrays (updated for all chains at once in step())
+        self.fnext = np.full(nc, int(filter_index_start), dtype=np.int64)
+        self.filters_run = np.zeros(nc, dtype=np.int64)
         # per-chain host RNG entry points, looked up once (a step makes 3 calls per chain)
         self._normal = [r.standard_normal for r in self.rngs]
         self._uniform = [r.random_sample for r in self.rngs]
@@ -318,7 +357,19 @@ class ChainSampler:
         self._peek = None
         if nc <= self.FUSE_PATH_CHAINS and all(b is not None for b in self._raw):
             self._peek = [_MTPeek(b) for b in self._raw]
-        self.acceptances = [1] * nc
+        # more chains: the host draws of an iteration in C (epipf_mh_propose / epipf_mh_decide, csrc/host_mh.cpp) --
+        # legacy RandomStates the sampler drives alone, an even d (whole gaussian pairs), an empty gaussian cache,
+        # the log-space acceptance, and numpy's own dgemv at hand
+        self._host = None
+        if (host_draws and nc > self.FUSE_PATH_CHAINS and d % 2 == 0 and mh_ratio == "log"
+                and all(b is not None for b in self._raw) and len({id(b) for b in self._raw}) == nc
+                and all(int(r.get_state()[3]) == 0 for r in (np.random.mtrand._rand if r is np.random else r
+                                                            for r in self.rngs))
+                and _NumpyDgemv.pointer()):
+            self._host = (ctypes.c_void_p * nc)(*[b.ctypes.state_address for b in self._raw])
+            self._facs = np.zeros((nc, d, d))
+            self._facs_ok = False
+        self.acceptances = np.ones(nc, dtype=np.int64)
         self.dth = d - (1 if probs is None else 0)
         self.i = 0
         self.last_active = 0
@@ -421,12 +472,25 @@ class ChainSampler:
         # multivariate_normal(theta, h std) per chain (mvn_apply's arithmetic: np.dot(z, factor) per chain -- a
         # batched product would take another BLAS kernel and round differently -- then + theta for all chains)
         D, fac, normal = self._dbuf, self._fac, self._normal
-        for c in range(nc):
-            f = fac[c]
-            if f is None:
-                f = fac[c] = mvn_factor(self.h * self.std[c])
-            np.dot(normal[c](d).reshape(1, d), f, out=D[c:c + 1])
-        P = D + self.thetas[:, i - 1]
+        if self._host is not None:
+            for c in range(nc):
+                if fac[c] is None:
+                    fac[c] = mvn_factor(self.h * self.std[c])
+                    self._facs_ok = False
+            if not self._facs_ok:
+                self._facs[:] = np.stack(fac)
+                self._facs_ok = True
+            mean = np.ascontiguousarray(self.thetas[:, i - 1])
+            P = np.empty((nc, d))
+            _lib.check(_lib.load().epipf_mh_propose(nc, d, self._host, _lib.ptr(self._facs), _lib.ptr(mean),
+                                                    _lib.ptr(P), _NumpyDgemv.pointer()), "epipf_mh_propose")
+        else:
+            for c in range(nc):
+                f = fac[c]
+                if f is None:
+                    f = fac[c] = mvn_factor(self.h * self.std[c])
+                np.dot(normal[c](d).reshape(1, d), f, out=D[c:c + 1])
+            P = D + self.thetas[:, i - 1]
         live = ~(P < 0).any(axis=1)                               # sum(prop < 0) > 0: no filter, :333-337
         lv = np.flatnonzero(live)
         acc = np.zeros(0, dtype=np.intp)
@@ -437,10 +501,9 @@ class ChainSampler:
             else:
                 th_all, pr_all, new_all = P, np.full(nc, float(self.probs)), P
             fidx = np.zeros(nc, dtype=np.uint64)
-            for c in lv.tolist():
-                fidx[c] = self.fnext[c]
-                self.fnext[c] += 1
-                self.filters_run[c] += 1
+            fidx[lv] = self.fnext[lv]
+            self.fnext[lv] += 1
+            self.filters_run[lv] += 1
             self._bind()
             pre = None
             if self._peek is not None:                            # the path pick, peeked (see _MTPeek)
@@ -456,7 +519,23 @@ class ChainSampler:
             lz, st = out[0], out[1]
             self.last_active = int(lv.size)
             ok = np.flatnonzero(live & (st == _lib.STATUS_OK))    # degenerate filters: rejected, :365-369
-            if ok.size:
+            if ok.size and self._host is not None:            # picks and acceptance uniforms in C, in order
+                chosen = np.zeros(nc, dtype=np.int32)
+                acc_f = np.zeros(nc, dtype=np.int32)
+                lzT = np.ascontiguousarray(lz[:, -1])
+                old = np.ascontiguousarray(self.loglik[:, i - 1])
+                _lib.check(_lib.load().epipf_mh_decide(ok.size, _lib.ptr(ok.astype(np.int32)), self._host, self.N,
+                                                       _lib.ptr(lzT), _lib.ptr(old), _lib.ptr(chosen),
+                                                       _lib.ptr(acc_f)), "epipf_mh_decide")
+                tr = self.eng.path_sample(chosen)
+                acc = ok[acc_f[ok] == 1]
+                self.acceptances[acc] += 1
+                if acc.size:
+                    self.thetas[acc, i] = new_all[acc]
+                    self.loglik[acc, i] = lzT[acc]
+                    self.likelihoods[acc, i] = np.exp(lzT[acc])
+                    self._tr[acc, i] = tr[acc]
+            elif ok.size:
                 okl = ok.tolist()
                 if pre is None:
                     tr = self._path_sample(okl)
@@ -523,8 +602,8 @@ class ChainSampler:
         return self.results()
 
     def results(self):
-        return [ChainResult(self.thetas[c], self.likelihoods[c], self.loglik[c], self.trajs[c], self.acceptances[c],
-                            self.filters_run[c]) for c in range(self.nc)]
+        return [ChainResult(self.thetas[c], self.likelihoods[c], self.loglik[c], self.trajs[c],
+                            int(self.acceptances[c]), int(self.filters_run[c])) for c in range(self.nc)]
 
 
 def run_pipelined(samplers, steps):

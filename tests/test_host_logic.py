@@ -130,3 +130,32 @@ def test_random_sample_is_legacy_uniform():
     x = np.random.uniform()
     np.random.seed(4)
     assert np.random.random_sample() == x
+
+
+@pytest.mark.parametrize("probs", [0.1, None])
+def test_c_host_draws_equal_the_python_loop(datasets_golden, probs):
+    """More than FUSE_PATH_CHAINS chains take the C host draws (epipf_mh_propose / epipf_mh_decide, csrc/host_mh.cpp):
+    thetas, likelihoods, trajectories, counters and every chain's final RandomState equal the Python loop's
+    (host_draws=False).  probs=None: d = 3, odd, so that run keeps the Python loop -- checked too."""
+    from oracle_engine import OracleEngine
+    Y = datasets_golden["cfg1_binom"][:6]
+    nc = 20
+    params = [2.0, 1.0] if probs is not None else [2.0, 1.0, 0.1]
+    kw = dict(Y=Y, type_model="sir", parameters=params, h=0.05, iters=12, probs=probs, n_particles=12,
+              n_population=200, mu=20, mh_ratio="log")
+    runs = []
+    for hd in (True, False):
+        rngs = [np.random.RandomState(50 + c) for c in range(nc)]
+        s = pm.ChainSampler(**kw, rngs=rngs, keys=[pm.chain_key(50, c) for c in range(nc)],
+                            engine=OracleEngine(0, 1, 12, 6, nc), host_draws=hd)
+        assert (s._host is not None) == (hd and probs is not None)
+        res = s.run()
+        runs.append((res, [r.get_state() for r in rngs]))
+    (ra, sa), (rb, sb) = runs
+    for a, b in zip(ra, rb):
+        np.testing.assert_array_equal(a.thetas, b.thetas)
+        np.testing.assert_array_equal(a.log_likelihoods, b.log_likelihoods)
+        np.testing.assert_array_equal(a.sampled_trajs, b.sampled_trajs)
+        assert a.acceptances == b.acceptances and a.filters_run == b.filters_run
+    for u, v in zip(sa, sb):
+        assert np.array_equal(u[1], v[1]) and u[2:] == v[2:]

@@ -64,3 +64,62 @@ def test_proposal_into_a_buffer_equals_mvn_apply(d):
     P = D + M
     for c in range(64):
         np.testing.assert_array_equal(P[c], mvn_apply(Z[c].copy(), fac, M[c]))
+
+
+def _states(rngs):
+    import ctypes
+    return (ctypes.c_void_p * len(rngs))(*[r._bit_generator.ctypes.state_address for r in rngs])
+
+
+@pytest.mark.parametrize("d", [2, 4, 6])
+def test_c_proposals_equal_numpys_multivariate_normal(d):
+    """epipf_mh_propose (csrc/host_mh.cpp) against RandomState.standard_normal + mvn_apply on copies of the same
+    states: the proposals and the generators' positions afterwards (the next draws) are identical."""
+    from epipf import _lib
+    from epipf.pmcmc import _NumpyDgemv
+    dg = _NumpyDgemv.pointer()
+    if not dg:
+        pytest.skip("numpy's cblas_dgemv not found / not reproducing np.dot")
+    L = _lib.load()
+    nc = 40
+    rs = np.random.RandomState(d)
+    facs = np.stack([mvn_factor(0.01 * (lambda A: A @ A.T)(rs.standard_normal((d, d)))) for _ in range(nc)])
+    means = rs.standard_normal((nc, d))
+    a = [np.random.RandomState(100 + c) for c in range(nc)]
+    b = [np.random.RandomState(100 + c) for c in range(nc)]
+    for x, y in zip(a, b):                               # states at different positions, regenerations included
+        k = int(rs.randint(0, 700)) * 2
+        x.random_sample(k)
+        y.random_sample(k)
+    for it in range(30):
+        P = np.empty((nc, d))
+        _lib.check(L.epipf_mh_propose(nc, d, _states(a), _lib.ptr(facs), _lib.ptr(means), _lib.ptr(P), dg), "propose")
+        for c in range(nc):
+            np.testing.assert_array_equal(P[c], mvn_apply(b[c].standard_normal(d), facs[c], means[c]))
+    for x, y in zip(a, b):
+        assert x.random_sample() == y.random_sample()
+
+
+def test_c_picks_and_acceptance_equal_the_python_loop():
+    """epipf_mh_decide against legacy randint + random_sample + _log_ratio, for a subset of chains in order (NaN and
+    +-inf log-likelihoods included)."""
+    from epipf import _lib
+    from epipf.pmcmc import _log_ratio
+    L = _lib.load()
+    nc, N = 50, 977
+    rs = np.random.RandomState(9)
+    a = [np.random.RandomState(7 * c + 1) for c in range(nc)]
+    b = [np.random.RandomState(7 * c + 1) for c in range(nc)]
+    for it in range(40):
+        ok = np.sort(rs.choice(nc, int(rs.randint(1, nc)), replace=False)).astype(np.int32)
+        new = rs.normal(-50, 3, nc)
+        old = rs.normal(-50, 3, nc)
+        new[rs.randint(0, nc)] = np.nan
+        old[rs.randint(0, nc)] = -np.inf
+        chosen = np.zeros(nc, dtype=np.int32)
+        acc = np.zeros(nc, dtype=np.int32)
+        _lib.check(L.epipf_mh_decide(ok.size, _lib.ptr(ok), _states(a), N, _lib.ptr(new), _lib.ptr(old),
+                                     _lib.ptr(chosen), _lib.ptr(acc)), "decide")
+        for c in ok.tolist():
+            assert chosen[c] == legacy_randint(b[c], N)
+            assert acc[c] == int(b[c].random_sample() < _log_ratio(new[c], old[c]))

@@ -64,7 +64,7 @@ def _assert_same(a, b):
         np.testing.assert_array_equal(x.sampled_trajs, y.sampled_trajs)
         assert x.acceptances == y.acceptances
         assert x.filters_run == y.filters_run
-    assert sa.fnext == sb.fnext
+    assert list(sa.fnext) == list(sb.fnext)
     for u, v in zip(sta, stb):                     # the host RandomState ends in the same state
         assert u[0] == v[0] and np.array_equal(u[1], v[1]) and u[2:] == v[2:]
 
