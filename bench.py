@@ -463,7 +463,7 @@ def config_runs(ctx, args):
         from epipf import datasets
         Yc, mc = datasets.benchmark_dataset(cfg)
         # host-bound MH steps (config 1: N x T = 5,000 per filter): two chain groups' host work overlaps (main())
-        pipelines = 2 if chains > 1 and mc["N"] * Yc.shape[0] <= 20000 else 1
+        pipelines = (args.pipelines or 2) if chains > 1 and mc["N"] * Yc.shape[0] <= 20000 else 1
         if cfg == 1:
             steps *= 10                                                # 2-3 ms MH steps: time a few hundred ms
         entry = None
