@@ -61,8 +61,8 @@ def parse():
                     help="CPU baseline per `configs` workload: seconds of port filters at 1 thread and at all threads")
     ap.add_argument("--pipelines", type=int, default=int(os.environ.get("EPIPF_BENCH_PIPELINES", 0)),
                     help="chain groups on their own engine + host thread, so each group's MH host work overlaps the "
-                         "others' filters (epipf.pmcmc.run_pipelined); 1 = one lockstep sampler; 0 = automatic: 2 "
-                         "where the MH step is host-bound (config 1: tiny filters), else 1 (DESIGN.md §6)")
+                         "others' filters (epipf.pmcmc.run_pipelined); 0 / 1 = one lockstep sampler (config 1's host "
+                         "draws run in C since round 5, and two pipelines measured no faster, DESIGN.md §7)")
     ap.add_argument("--prefetch", type=int, default=16, help="filter slots per round of the speculative single chain")
     # ~40 rounds: a speculative round commits ~8 iterations at config 2; 60 iterations (6 rounds) moved the adaptive
     # width's figure by +-20% from run to run (profiles/r4y_prefetch_cfg5.txt), 200 still by ~+-7% (BENCH_r05)
@@ -463,13 +463,15 @@ def config_runs(ctx, args):
         from epipf import datasets
         Yc, mc = datasets.benchmark_dataset(cfg)
         # host-bound MH steps (config 1: N x T = 5,000 per filter): two chain groups' host work overlaps (main())
-        pipelines = (args.pipelines or 2) if chains > 1 and mc["N"] * Yc.shape[0] <= 20000 else 1
+        # config 1 (N x T = 5,000 per filter): one-workgroup filters and the host draws in C; --pipelines > 1 overlaps
+        # chain groups' host work with each other's filters (run_pipelined) -- measured no better since (r5q)
+        pipelines = (args.pipelines or 1) if chains > 1 and mc["N"] * Yc.shape[0] <= 20000 else 1
         if cfg == 1:
             steps *= 10                                                # 2-3 ms MH steps: time a few hundred ms
         entry = None
-        # N <= 256 (config 1): the engine's first six runs of a batch size time the one-workgroup filter against the
+        # N <= 256 (config 1): the engine's first eight runs of a batch size time the one-workgroup filter against the
         # step launches (EPIPF_FUSED=auto, epipf_api.cpp): warm up past them
-        warm = 8 if mc["N"] <= 256 else (1 if chains > 1 else 2)
+        warm = 10 if mc["N"] <= 256 else (1 if chains > 1 else 2)
         for kind in ("config", "fixed_theta"):
             run = timed_chains(ctx, args, cfg, chains, steps, warm, kind, pipelines=pipelines)
             run["cfg"] = cfg
@@ -552,7 +554,7 @@ def main():
     from epipf import datasets
     Y, meta0 = datasets.benchmark_dataset(args.config)
     N0, T0 = (args.particles or meta0["N"]), Y.shape[0]
-    pipelines = args.pipelines or (2 if N0 * T0 <= 20000 else 1)   # host-bound MH steps: overlap two samplers' host work
+    pipelines = args.pipelines or 1                  # > 1: chain groups' host work overlapping (run_pipelined)
     streams_env = max(1, min(int(os.environ.get("EPIPF_STREAMS", 4)), 8))
     run = timed_chains(ctx, args, args.config, C, args.steps, args.warmup, args.proposal, pipelines, streams_env)
     run["cfg"] = args.config

@@ -7,7 +7,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -124,8 +123,8 @@ struct epipf_ctx {
     // Which path is faster depends on the events per particle-step, which the host cannot see ahead: one workgroup per
     // chain wins where a step is little work or many chains fill the chip (config 1, N = 100, 6 events: 3.1x at 256
     // chains, 1.3x at one), the step launches where one chain's many events want more than one CU (N = 100 at config
-    // 2's 90 events: 2.2x the other way).  So a batch size's first runs time both (wall clock of epipf_run, results
-    // identical either way) and the faster one stays.
+    // 2's 90 events: 2.2x the other way).  So a batch size's first runs time both (the filter's device span, HIP
+    // events; results identical either way) and the faster one stays.
     struct FusedTune {
         int runs = 0;
         double best[2] = {1e300, 1e300};   // fastest timed run: [0] step launches, [1] one-workgroup filter
@@ -181,8 +180,9 @@ static int pick_fused(const epipf_ctx* c) {
     return 1;
 }
 
-// EPIPF_FUSED=auto (the default): runs 0-3 of a batch size alternate the paths (fused first, each path's first run
-// untimed), then the faster one's fastest timed run decides.  *timed: this run's wall time is recorded.
+// EPIPF_FUSED=auto (the default): runs 0-7 of a batch size alternate the paths (fused first, each path's first run
+// untimed), then each path's fastest of three timed runs decides, the step launches only by a 15% margin (concurrent
+// contexts -- run_pipelined -- share the device while they time, which spreads both paths' times).  *timed: this run's wall time is recorded.
 static bool fused_decide(epipf_ctx* c, int n_chains, bool& timed) {
     timed = false;
     if (c->fused >= 0) return c->fused == 1;
@@ -195,7 +195,7 @@ static bool fused_decide(epipf_ctx* c, int n_chains, bool& timed) {
 static void fused_record(epipf_ctx* c, int n_chains, bool fused, double seconds) {
     epipf_ctx::FusedTune& t = c->fused_tune[n_chains];
     t.best[fused ? 1 : 0] = std::min(t.best[fused ? 1 : 0], seconds);
-    if (++t.runs >= 6) t.choice = t.best[1] <= t.best[0] ? 1 : 0;
+    if (++t.runs >= 8) t.choice = t.best[0] < 0.85 * t.best[1] ? 0 : 1;
 }
 
 static hipError_t launch_fused_run(const StepArgs& a, const epipf_ctx* c, int obs, int n_chains, const FilterStreams& fs) {
@@ -510,7 +510,6 @@ static int run_impl(epipf_ctx* c, int n_chains, const double* theta, int d, int 
     bool tune_timed = false;
     const int fusedW = pick_fused(c) && fused_decide(c, n_chains, tune_timed) ? pick_fused(c) : 0;
     const bool tuning = pick_fused(c) && c->fused < 0 && c->fused_tune[n_chains].choice < 0;
-    const auto t_start = std::chrono::steady_clock::now();
     a.lanes = fusedW ? fusedW : pick_lanes(c, n_chains);
     a.wg = fusedW ? 64 : pick_block(c, a.lanes);
     a.B = (c->N + a.wg - 1) / a.wg;
@@ -562,9 +561,9 @@ static int run_impl(epipf_ctx* c, int n_chains, const double* theta, int d, int 
         fs.join[g] = c->join[g];
         HIP_TRY(hipStreamWaitEvent(c->aux[g], c->fork, 0));
     }
-    fs.ev_init = c->profiling ? c->ev[0] : nullptr;
+    fs.ev_init = (c->profiling || tuning) ? c->ev[0] : nullptr;   // the path choice times the device span
     fs.ev_step0 = c->profiling ? c->ev[1] : nullptr;
-    fs.ev_end = c->profiling ? c->ev[2] : nullptr;
+    fs.ev_end = (c->profiling || tuning) ? c->ev[2] : nullptr;
     for (int g = 0; g < fs.n; ++g) {
         fs.g_begin[g] = c->profiling ? c->gb[g] : nullptr;
         fs.g_end[g] = c->profiling ? c->ge[g] : nullptr;
@@ -588,9 +587,11 @@ static int run_impl(epipf_ctx* c, int n_chains, const double* theta, int d, int 
     HIP_TRY(hipMemcpyAsync(c->h_res, c->res, c->res_lz + sizeof(double) * (size_t)n_chains * c->T, hipMemcpyDeviceToHost,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (tuning) {
-        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
-        fused_record(c, n_chains, fusedW != 0, tune_timed ? dt : 1e300);
+    if (tuning) {   // the filter's device span, init to the last step (host threads contending for the GIL do not
+                    // enter it, as they would a wall clock)
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[2]));
+        fused_record(c, n_chains, fusedW != 0, tune_timed ? (double)ms : 1e300);
     }
     if (chosen) memcpy(traj_out, c->h_traj, sizeof(int32_t) * (size_t)n_chains * c->T * c->C);
     memcpy(status_out, c->h_status, sizeof(int32_t) * n_chains);

@@ -256,7 +256,7 @@ def test_run_sampled_equals_run_then_path_sample(datasets_golden, N):
 
 
 def test_automatic_choice_times_both_paths_with_identical_results(datasets_golden, monkeypatch):
-    """EPIPF_FUSED=auto (the default): a batch size's first six runs alternate the one-workgroup filter and the step
+    """EPIPF_FUSED=auto (the default): a batch size's first eight runs alternate the one-workgroup filter and the step
     launches (fused first), then one path stays; every run's outputs are the same."""
     from epipf.engine import Engine
     monkeypatch.setenv("EPIPF_FUSED", "auto")
@@ -266,13 +266,13 @@ def test_automatic_choice_times_both_paths_with_identical_results(datasets_golde
     eng.set_population(c["npop"], c["mu"])
     th = np.tile([4.0, 1.0, 1.0], (3, 1))
     used, outs = [], []
-    for r in range(9):
+    for r in range(11):
         lz, st = eng.run(th, [0.1] * 3, [1, 2, 3], [5, 5, 5])
         used.append(eng.stats()["last_fused"])
         outs.append((lz.copy(), st.copy(), *eng.history(3)))
     eng.close()
-    assert used[:6] == [1, 0, 1, 0, 1, 0]
-    assert len(set(used[6:])) == 1
+    assert used[:8] == [1, 0, 1, 0, 1, 0, 1, 0]
+    assert len(set(used[8:])) == 1
     for o in outs[1:]:
         for x, y in zip(o, outs[0]):
             np.testing.assert_array_equal(x, y)
