@@ -72,6 +72,13 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise EpipfError(f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
                          "(the HIP path has no CPU fallback)")
+    # One HIP runtime per process: torch (device memory, streams, RCCL for the multi-GPU gather) ships its own
+    # libamdhip64 / ROCr.  Loaded first, the library's HIP dependency resolves to that same runtime; loaded after
+    # libepipf's, torch's second runtime finds no GPU ("No HIP GPUs are available", scripts/torch_after_epipf.py).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     P = ctypes.c_void_p
     i32, u32, u64, f64 = ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double

@@ -79,6 +79,7 @@ class Engine:
         self._L = L
         self._Y = None
         self._pop = None
+        self.bound_to = None                             # the ChainSampler whose data is loaded (ChainSampler._bind)
         self.T = 0
 
     # ------------------------------------------------------------------ lifecycle
@@ -102,6 +103,7 @@ class Engine:
             return
         check(self._L.epipf_set_observations(self._h, ptr(Y), Y.shape[0], Y.shape[1]), "epipf_set_observations")
         self._Y = Y.copy()
+        self.bound_to = None                             # ChainSampler._bind: the data it bound is gone
         self.T = Y.shape[0]
 
     def set_population(self, n_population, mu):
@@ -114,6 +116,7 @@ class Engine:
             return
         check(self._L.epipf_set_population(self._h, ptr(npop), ptr(mus)), "epipf_set_population")
         self._pop = key
+        self.bound_to = None
 
     # ------------------------------------------------------------------ the filter
     def run(self, thetas, probs, keys, filter_indices, observations=False, active=None, resample="multinomial",

@@ -378,8 +378,11 @@ class ChainSampler:
         """(Re)load this sampler's observations and population into its engine before a run: a cached engine is
         shared with every other sampler / particle_filter call of the same model, N and device (no-op when
         unchanged, engine.set_observations / set_population compare first)."""
+        if getattr(self.eng, "bound_to", None) is self:   # nothing re-uploaded the engine's data since this sampler's
+            return
         self.eng.set_observations(self._Y)
         self.eng.set_population(self._npop, self._mus)
+        self.eng.bound_to = self
 
     def _propose(self, c, mean):
         """rngs[c].multivariate_normal(mean, h * std[c]) (pmcmc.py:277, :330) with the SVD factor cached per chain."""
@@ -458,11 +461,84 @@ class ChainSampler:
             pending = [c for c in pending if c not in ok]
         self.i = 1
 
+    def _step_one(self):
+        """step() for a single chain (particle_mcmc; BASELINE config 5's one chain per GPU) on plain Python scalars:
+        the batched step's ~30 small numpy calls cost ~50-90 us an iteration, ~7% of a config-5 one-chain MH
+        iteration, between two filters.  Same RNG calls in the same order, same arithmetic (the proposal's np.dot and
+        + theta; the log- or reference-ratio acceptance), same bookkeeping."""
+        i, d = self.i, self.d
+        if self.adaptive and i > 1e3:
+            self.std[0] = np.cov(self.thetas[0, :i].T, ddof=0) + 1e-4 * np.eye(self.d)
+            self._fac[0] = None
+        f = self._fac[0]
+        if f is None:
+            f = self._fac[0] = mvn_factor(self.h * self.std[0])
+        D = self._dbuf
+        np.dot(self._normal[0](d).reshape(1, d), f, out=D)
+        prop = D[0] + self.thetas[0, i - 1]
+        pl = prop.tolist()
+        ran = 0
+        take = False
+        if not any(v < 0 for v in pl):                            # sum(prop < 0) > 0: no filter, :333-337
+            ran = 1
+            if self.probs is None:                                # :339-346: the last entry is probs
+                p2 = min(max(pl[-1], 0.0), 1.0)
+                th = prop[:-1]
+                new = pl[:-1] + [p2]
+            else:
+                p2 = float(self.probs)
+                th = prop
+                new = pl
+            fidx = int(self.fnext[0])
+            self.fnext[0] += 1
+            self.filters_run[0] += 1
+            self._bind()
+            pre = None
+            if self._peek is not None:                            # the path pick, peeked (see _MTPeek)
+                v = self._peek[0].randint(self.N)
+                if v is not None:
+                    pre = [v]
+            out = self.eng.run(th[None, :], [p2], self.keys, [fidx], observations=self.observations,
+                               resample=self.resample, chosen=pre)
+            self.last_active = 1
+            if int(out[1][0]) == _lib.STATUS_OK:                  # degenerate filters: rejected, :365-369
+                real = legacy_randint(self.rngs[0], self.N, self._raw[0])
+                if pre is None:
+                    chosen = np.array([real], dtype=np.int32)
+                    tr = self.eng.path_sample(chosen)[0]
+                elif real == pre[0]:
+                    tr = out[2][0]
+                else:                                             # (never seen) walk the drawn pick instead
+                    self._peek = None
+                    tr = self.eng.path_sample(np.array([real], dtype=np.int32))[0]
+                lzT = float(out[0][0, -1])
+                if self.mh_ratio == "reference":
+                    prob = _reference_ratio(np.exp(out[0][0, -1]), self.likelihoods[0, i - 1], np.array(new),
+                                            self.thetas[0, i - 1], self.params[0], self.h * self.std[0])
+                else:
+                    prob = _log_ratio(lzT, float(self.loglik[0, i - 1]))
+                if self._uniform[0]() < prob:
+                    take = True
+                    self.acceptances[0] += 1
+                    self.thetas[0, i] = new
+                    self.loglik[0, i] = lzT
+                    self.likelihoods[0, i] = np.exp(out[0][0, -1])
+                    self._tr[0, i] = tr
+        if not take:                                              # rejected, negative or degenerate: previous row
+            self.thetas[0, i] = self.thetas[0, i - 1]
+            self.likelihoods[0, i] = self.likelihoods[0, i - 1]
+            self.loglik[0, i] = self.loglik[0, i - 1]
+            self._tr[0, i] = self._tr[0, i - 1]
+        self.i += 1
+        return ran
+
     def step(self):
         """One MH iteration for every chain, pmcmc.py:325-406.  Returns the number of chains that ran a filter.
         Per chain the RNG calls keep the reference's order (proposal normals, path-pick randint, acceptance
         uniform); everything else -- the negative-proposal test, the batch arrays, the accepted rows and the copies
         of the previous row -- is one array operation over the chains."""
+        if self.nc == 1:
+            return self._step_one()
         i = self.i
         nc, d = self.nc, self.d
         if self.adaptive and i > 1e3:
