@@ -469,9 +469,9 @@ def config_runs(ctx, args):
         if cfg == 1:
             steps *= 10                                                # 2-3 ms MH steps: time a few hundred ms
         entry = None
-        # N <= 256 (config 1): the engine's first eight runs of a batch size time the one-workgroup filter against the
+        # N <= 512 (config 1): the engine's first eight runs of a batch size time the one-workgroup filter against the
         # step launches (EPIPF_FUSED=auto, epipf_api.cpp): warm up past them
-        warm = 10 if mc["N"] <= 256 else (1 if chains > 1 else 2)
+        warm = 10 if mc["N"] <= 512 else (1 if chains > 1 else 2)
         for kind in ("config", "fixed_theta"):
             run = timed_chains(ctx, args, cfg, chains, steps, warm, kind, pipelines=pipelines)
             run["cfg"] = cfg

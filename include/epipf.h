@@ -96,7 +96,7 @@ typedef struct {
                                        weights (within the measured envelope of their error) could pick
                                        a neighbouring ancestor: a diagnostic count, always on; the draw itself is the
                                        numpy answer over the device's weights */
-    int64_t last_fused;          /* 1: the last epipf_run ran each chain's whole filter in one workgroup launch (N <= 256
+    int64_t last_fused;          /* 1: the last epipf_run ran each chain's whole filter in one workgroup launch (N <= 512
                                     with the lanes automatic); 0: one launch per filter step */
 } epipf_stats;
 

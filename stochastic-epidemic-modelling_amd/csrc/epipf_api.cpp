@@ -172,12 +172,13 @@ static int pick_block(const epipf_ctx* c, int W) {
 }
 
 // Lanes per particle of the one-workgroup filter (epipf_fused.hpp), or 0 when the run takes the step launches: N <=
-// kFusedMaxN with the lanes automatic (an explicit epipf_set_lanes / EPIPF_LANES keeps the step kernels it names).  W is
-// the widest of 16 / 8 / 4 / 2 whose N W lanes fit one workgroup.
+// kFusedMaxN with the lanes automatic (an explicit epipf_set_lanes / EPIPF_LANES keeps the step kernels it names) and
+// the chain's LDS within the default launch limit.  W: EPIPF_FUSED_LANES where its N W lanes fit one workgroup, else 1.
 static int pick_fused(const epipf_ctx* c) {
     if (!c->fused || c->lanes > 0 || c->N > kFusedMaxN) return 0;
-    if (c->fused_lanes > 0 && c->N * c->fused_lanes <= kFusedMaxThreads) return c->fused_lanes;
-    return 1;
+    const int W = (c->fused_lanes > 0 && c->N * c->fused_lanes <= kFusedMaxThreads) ? c->fused_lanes : 1;
+    if (fused_lds_bytes_of(c->N, c->C, fused_threads_of(c->N, W), 0, 0) > kFusedLdsLimit) return 0;
+    return W;
 }
 
 // EPIPF_FUSED=auto (the default): runs 0-7 of a batch size alternate the paths (fused first, each path's first run

@@ -198,7 +198,7 @@ hipError_t launch_filter(const StepArgs& a, int model, int G, int obs, int n_cha
 // the one-workgroup filter (epipf_fused.hpp): init and every step of a chain in one launch, for N <= kFusedMaxN;
 // one workgroup of fused_threads(N, W) threads per chain, W lanes per particle in the SSA
 constexpr int kFusedMaxThreads = 512;    // 8 waves: up to 256 VGPRs a lane (2 waves per SIMD)
-constexpr int kFusedMaxN = 256;
+constexpr int kFusedMaxN = 512;     // N lanes of one particle each in a 512-thread workgroup
 constexpr size_t kFusedLdsLimit = 64 * 1024;    // the default dynamic LDS limit of a launch
 using FusedFn = void (*)(const StepArgs& a, int n_chains, int threads, size_t lds, hipStream_t s);
 FusedFn fused_launcher(int model, int G, int obs, int W);

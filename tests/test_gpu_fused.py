@@ -72,7 +72,7 @@ def _run_both(monkeypatch, *args, **kw):
 
 
 @pytest.mark.parametrize("lanes", [0, 1, 2, 4, 16])
-@pytest.mark.parametrize("N", [1, 37, 64, 100, 129, 200, 256])
+@pytest.mark.parametrize("N", [1, 37, 64, 100, 129, 200, 256, 300, 512])
 @pytest.mark.parametrize("model", MODELS)
 def test_fused_filter_matches_oracle(datasets_golden, monkeypatch, model, N, lanes):
     """Every SSA width of the one-workgroup filter (EPIPF_FUSED_LANES, read at create; 0: the automatic one)."""
@@ -97,11 +97,11 @@ def test_fused_filter_matches_oracle(datasets_golden, monkeypatch, model, N, lan
 
 
 def test_fused_threshold_and_explicit_lanes(datasets_golden, monkeypatch):
-    """N = 257 and explicit lanes (epipf_set_lanes / EPIPF_LANES) take the step launches; EPIPF_FUSED=0 switches the
+    """N = 513 and explicit lanes (epipf_set_lanes / EPIPF_LANES) take the step launches; EPIPF_FUSED=0 switches the
     one-workgroup filter off."""
     from epipf.engine import Engine
     c = _case(datasets_golden, "sir")
-    for N, lanes, env, want in [(256, 0, None, 1), (257, 0, None, 0), (100, 4, None, 0), (100, 0, "0", 0)]:
+    for N, lanes, env, want in [(512, 0, None, 1), (513, 0, None, 0), (100, 4, None, 0), (100, 0, "0", 0)]:
         if env is not None:
             monkeypatch.setenv("EPIPF_FUSED", env)
         eng = Engine("sir", 1, N, c["Y"].shape[0], 1)
@@ -276,3 +276,30 @@ def test_automatic_choice_times_both_paths_with_identical_results(datasets_golde
     for o in outs[1:]:
         for x, y in zip(o, outs[0]):
             np.testing.assert_array_equal(x, y)
+
+
+def test_many_chain_host_draws_on_the_device_engine(datasets_golden, monkeypatch):
+    """24 chains of the config-1 shape (N = 100: the one-workgroup filter) through ChainSampler with the C host draws
+    (epipf_mh_propose / epipf_mh_decide) and with the Python loop: identical thetas, likelihoods, paths, counters and
+    final generator states."""
+    from epipf import pmcmc as pm
+    monkeypatch.setenv("EPIPF_FUSED", "auto")
+    Y = datasets_golden["cfg1_binom"][:20]
+    nc = 24
+    runs = []
+    for hd in (True, False):
+        rngs = [np.random.RandomState(300 + c) for c in range(nc)]
+        s = pm.ChainSampler(Y, "sir", [2.0, 1.0], 0.02, iters=15, probs=0.1, n_particles=100, n_population=200, mu=20,
+                            rngs=rngs, keys=[pm.chain_key(300, c) for c in range(nc)], mh_ratio="log", host_draws=hd,
+                            engine_chains=nc)
+        assert (s._host is not None) == hd
+        res = s.run()
+        runs.append((res, [r.get_state() for r in rngs]))
+    (ra, sa), (rb, sb) = runs
+    for a, b in zip(ra, rb):
+        np.testing.assert_array_equal(a.thetas, b.thetas)
+        np.testing.assert_array_equal(a.log_likelihoods, b.log_likelihoods)
+        np.testing.assert_array_equal(a.sampled_trajs, b.sampled_trajs)
+        assert a.acceptances == b.acceptances and a.filters_run == b.filters_run
+    for u, v in zip(sa, sb):
+        assert np.array_equal(u[1], v[1]) and u[2:] == v[2:]
