@@ -229,6 +229,9 @@ int epipf_mh_propose(int n_chains, int d, void* const* mt_states, const double* 
                      double* props_out, void* dgemv);
 int epipf_mh_decide(int n, const int32_t* chains, void* const* mt_states, int n_particles, const double* lz_new,
                     const double* lz_old, int32_t* chosen_out, int32_t* accept_out);
+/* epipf_mh_peek: chosen_out[c] = the randint(0, n_particles) the next epipf_mh_decide draws for each listed chain,
+ * read on a copy of its state (nothing consumed): the path sampler's picks for epipf_run_sampled, before the filter. */
+int epipf_mh_peek(int n, const int32_t* chains, void* const* mt_states, int n_particles, int32_t* chosen_out);
 
 const char* epipf_last_error(void);
 int epipf_abi_version(void);

@@ -15,9 +15,12 @@
 //   randint(0, N)   masked rejection on 32-bit words (random_bounded_uint64_fill's buffered_bounded_masked_uint32)
 //   multivariate_normal's np.dot(z, factor): the same OpenBLAS routine numpy calls for a (1, d) x (d, d) product
 //                   (cblas_dgemv, row-major, transposed), passed in by the caller from numpy's own library
+// epipf_mh_peek: the randint(0, N) the next epipf_mh_decide will draw, without consuming it (a copy of the state),
+// so that the path sampler can ride on the filter's launch (epipf_run_sampled) for any number of chains.
 // Compiled without FMA contraction (-ffp-contract=off), like numpy's baseline build of these functions.
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 
 #include "../../include/epipf.h"
 
@@ -105,6 +108,18 @@ int epipf_mh_propose(int n_chains, int d, void* const* mt_states, const double* 
         for (int k = 0; k < d; k += 2) gauss_pair(s, z[k], z[k + 1]);            // standard_normal(d)
         gemv(kRowMajor, kTrans, d, d, 1.0, factors + (size_t)c * d * d, d, z, 1, 0.0, y, 1);   // np.dot(z, factor)
         for (int k = 0; k < d; ++k) props_out[(size_t)c * d + k] = y[k] + means[(size_t)c * d + k];   // += mean
+    }
+    return EPIPF_OK;
+}
+
+int epipf_mh_peek(int n, const int32_t* chains, void* const* mt_states, int n_particles, int32_t* chosen_out) {
+    if (n < 0 || n_particles < 1 || !chains || !mt_states || !chosen_out) return EPIPF_EINVAL;
+    for (int i = 0; i < n; ++i) {
+        const int c = chains[i];
+        const MTState* s = static_cast<const MTState*>(mt_states[c]);
+        MTState copy;                                     // the draw on a copy: the chain's state is not consumed
+        memcpy(&copy, s, sizeof copy);
+        chosen_out[c] = bounded(&copy, (uint32_t)(n_particles - 1));
     }
     return EPIPF_OK;
 }

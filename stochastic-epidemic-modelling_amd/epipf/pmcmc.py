@@ -367,6 +367,7 @@ class ChainSampler:
                                                             for r in self.rngs))
                 and _NumpyDgemv.pointer()):
             self._host = (ctypes.c_void_p * nc)(*[b.ctypes.state_address for b in self._raw])
+            self._host_peek = True
             self._facs = np.zeros((nc, d, d))
             self._facs_ok = False
         self.acceptances = np.ones(nc, dtype=np.int64)
@@ -590,6 +591,11 @@ class ChainSampler:
                         pre = None
                         break
                     pre[c] = v
+            elif self._host is not None and self._host_peek:     # many chains: peeked in C (epipf_mh_peek)
+                pre = np.full(nc, -1, dtype=np.int32)
+                lvc = lv.astype(np.int32)
+                _lib.check(_lib.load().epipf_mh_peek(lv.size, _lib.ptr(lvc), self._host, self.N, _lib.ptr(pre)),
+                           "epipf_mh_peek")
             out = self.eng.run(np.ascontiguousarray(th_all), pr_all, self.keys, fidx, observations=self.observations,
                                active=live.astype(np.int32), resample=self.resample, chosen=pre)
             lz, st = out[0], out[1]
@@ -603,7 +609,12 @@ class ChainSampler:
                 _lib.check(_lib.load().epipf_mh_decide(ok.size, _lib.ptr(ok.astype(np.int32)), self._host, self.N,
                                                        _lib.ptr(lzT), _lib.ptr(old), _lib.ptr(chosen),
                                                        _lib.ptr(acc_f)), "epipf_mh_decide")
-                tr = self.eng.path_sample(chosen)
+                if pre is not None and np.array_equal(chosen[ok], pre[ok]):
+                    tr = out[2]                                   # walked on the filter's stream
+                else:
+                    if pre is not None:                           # (never seen) walk the drawn picks instead
+                        self._host_peek = False
+                    tr = self.eng.path_sample(chosen)
                 acc = ok[acc_f[ok] == 1]
                 self.acceptances[acc] += 1
                 if acc.size:

@@ -123,3 +123,27 @@ def test_c_picks_and_acceptance_equal_the_python_loop():
         for c in ok.tolist():
             assert chosen[c] == legacy_randint(b[c], N)
             assert acc[c] == int(b[c].random_sample() < _log_ratio(new[c], old[c]))
+
+
+def test_c_peek_equals_the_next_decide_without_consuming():
+    """epipf_mh_peek gives the pick the next epipf_mh_decide draws and leaves the states untouched (positions at the
+    end of the 624-word state included, where the draw regenerates it)."""
+    from epipf import _lib
+    L = _lib.load()
+    nc, N = 30, 313
+    rs = np.random.RandomState(4)
+    a = [np.random.RandomState(11 * c + 2) for c in range(nc)]
+    for c, r in enumerate(a):
+        r.random_sample(311 + c)                         # words 622 + 2c: the next draw regenerates for the first few
+    for it in range(20):
+        ok = np.sort(rs.choice(nc, int(rs.randint(1, nc)), replace=False)).astype(np.int32)
+        before = [r.get_state()[1].copy() for r in a]
+        peek = np.full(nc, -1, dtype=np.int32)
+        _lib.check(L.epipf_mh_peek(ok.size, _lib.ptr(ok), _states(a), N, _lib.ptr(peek)), "peek")
+        assert all(np.array_equal(b, r.get_state()[1]) for b, r in zip(before, a))
+        chosen = np.zeros(nc, dtype=np.int32)
+        acc = np.zeros(nc, dtype=np.int32)
+        z = np.zeros(nc)
+        _lib.check(L.epipf_mh_decide(ok.size, _lib.ptr(ok), _states(a), N, _lib.ptr(z), _lib.ptr(z),
+                                     _lib.ptr(chosen), _lib.ptr(acc)), "decide")
+        np.testing.assert_array_equal(chosen[ok], peek[ok])
