@@ -114,12 +114,28 @@ int epipf_mh_propose(int n_chains, int d, void* const* mt_states, const double* 
 
 int epipf_mh_peek(int n, const int32_t* chains, void* const* mt_states, int n_particles, int32_t* chosen_out) {
     if (n < 0 || n_particles < 1 || !chains || !mt_states || !chosen_out) return EPIPF_EINVAL;
+    const uint32_t rng = (uint32_t)(n_particles - 1);
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
     for (int i = 0; i < n; ++i) {
         const int c = chains[i];
         const MTState* s = static_cast<const MTState*>(mt_states[c]);
-        MTState copy;                                     // the draw on a copy: the chain's state is not consumed
-        memcpy(&copy, s, sizeof copy);
-        chosen_out[c] = bounded(&copy, (uint32_t)(n_particles - 1));
+        int32_t v = -1;
+        if (rng == 0) v = 0;
+        for (int p = s->pos; v < 0 && p < kN; ++p) {     // the words ahead, read in place and tempered as next32 would
+            uint32_t y = s->key[p];
+            y ^= (y >> 11);
+            y ^= (y << 7) & 0x9d2c5680u;
+            y ^= (y << 15) & 0xefc60000u;
+            y ^= (y >> 18);
+            if ((y & mask) <= rng) v = (int32_t)(y & mask);
+        }
+        if (v < 0) {                                      // the draw regenerates the state first: on a copy
+            MTState copy;
+            memcpy(&copy, s, sizeof copy);
+            v = bounded(&copy, rng);
+        }
+        chosen_out[c] = v;
     }
     return EPIPF_OK;
 }
