@@ -693,12 +693,20 @@ class ChainSampler:
                             int(self.acceptances[c]), int(self.filters_run[c])) for c in range(self.nc)]
 
 
+PIPELINE_SWITCH_S = 1e-4
+
+
 def run_pipelined(samplers, steps):
     """Advance independent ChainSamplers `steps` MH iterations each, one host thread per sampler, and return the
     number of filters run.  Each sampler must own its engine (ChainSampler(..., engine=Engine(...))): a filter call
     releases the GIL for its whole device run (ctypes), so one sampler's host work (proposals, path picks,
     accept/reject) overlaps the other samplers' filters on the device instead of leaving it idle between MH
-    iterations.  Every sampler's chains, draws and results are exactly those of calling its step() `steps` times."""
+    iterations.  Every sampler's chains, draws and results are exactly those of calling its step() `steps` times.
+
+    While it runs, the interpreter's thread switch interval is at most PIPELINE_SWITCH_S: a thread back from a filter
+    call otherwise can wait out the default 5 ms for the GIL whenever the holder releases and retakes it within short
+    C calls -- whole-millisecond stalls in sub-millisecond MH iterations (profiles/r5v_cfg1_chains.jsonl)."""
+    import sys
     import threading
     engines = [id(s.eng) for s in samplers]
     if len(set(engines)) != len(engines):
@@ -714,10 +722,15 @@ def run_pipelined(samplers, steps):
             errors.append(e)
 
     threads = [threading.Thread(target=work, args=(k,), daemon=True) for k in range(len(samplers))]
-    for t in threads:
-        t.start()
-    for t in threads:
-        t.join()
+    switch = sys.getswitchinterval()
+    sys.setswitchinterval(min(switch, PIPELINE_SWITCH_S))
+    try:
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+    finally:
+        sys.setswitchinterval(switch)
     if errors:
         raise errors[0]
     return sum(counts)
