@@ -17,6 +17,7 @@ a PMC profile of that (config, chains, lanes) on this library build is committed
 CPU baseline with the reference-calibrated rate of that config (profiles/reference_timing_cfg<c>.json).
 """
 import argparse
+import gc
 import glob
 import json
 import os
@@ -487,6 +488,12 @@ def config_runs(ctx, args):
                 entry["proposal_kind"] = "config"
             else:
                 entry["fixed_theta"] = run_summary(run)
+            # release the leg's engines (their HIP streams) before the next one: idle contexts' streams still hold
+            # hardware queues, and the next leg's concurrent engines could be placed on a shared one
+            run["samplers"] = run["engines"] = None
+            gc.collect()
+        run["samplers"] = run["engines"] = None
+        gc.collect()
         if chains == 1 and ctx.rank == 0 and ctx.world == 1:
             # at the config's proposal (config 5: h = 1, acceptance often 0 over a segment: each round then commits about
             # as many iterations as it has slots) and at the near-fixed theta (acceptance ~0.6: the speculation tree's
