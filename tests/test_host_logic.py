@@ -2,6 +2,8 @@
 stand-in that answers from the oracle, so the accept/reject / RNG-order / probs=None / subgroup /
 adaptive logic is checked against the reference's own PMCMC runs (tests/golden/pmcmc_golden.npz)
 without a GPU.  The product has no such fallback: epipf.engine.Engine always requires libepipf + a GPU."""
+import sys
+
 import numpy as np
 import pytest
 
@@ -107,7 +109,9 @@ def test_pipelined_samplers_equal_one_lockstep_sampler(datasets_golden):
              for grp in groups]
     for s in parts:
         s.initialise()
+    switch = sys.getswitchinterval()
     assert pm.run_pipelined(parts, 6) == ran
+    assert sys.getswitchinterval() == switch          # lowered only while the threads run
     got = [r for s in parts for r in s.results()]
     for a, b in zip(whole.results(), got):
         np.testing.assert_array_equal(a.thetas, b.thetas)
