@@ -546,15 +546,15 @@ class ChainSampler:
             for c in range(nc):
                 self.std[c] = np.cov(self.thetas[c, :i].T, ddof=0) + 1e-4 * np.eye(self.d)
                 self._fac[c] = None
+            self._facs_ok = False
         # multivariate_normal(theta, h std) per chain (mvn_apply's arithmetic: np.dot(z, factor) per chain -- a
         # batched product would take another BLAS kernel and round differently -- then + theta for all chains)
         D, fac, normal = self._dbuf, self._fac, self._normal
         if self._host is not None:
-            for c in range(nc):
-                if fac[c] is None:
-                    fac[c] = mvn_factor(self.h * self.std[c])
-                    self._facs_ok = False
-            if not self._facs_ok:
+            if not self._facs_ok:                                 # factors (re)computed: start, adaptive update
+                for c in range(nc):
+                    if fac[c] is None:
+                        fac[c] = mvn_factor(self.h * self.std[c])
                 self._facs[:] = np.stack(fac)
                 self._facs_ok = True
             mean = np.ascontiguousarray(self.thetas[:, i - 1])
