@@ -11,7 +11,7 @@ all-gathered over RCCL at the end of the timed region (pmcmc chain gather, SURVE
 
 Also reported: roofline of the dominant kernel (pf_step_kernel, HIP-event timed on the engine's stream),
 a CPU baseline (the oracle C restatement, OpenMP, on a bounded sample) on rank 0 at N=1, and `configs`: short
-timed runs of the other BASELINE workloads -- config 1 at 3,072 chains per GPU, configs 3, 4, 5 at 256 and config 5 at ONE chain per
+timed runs of the other BASELINE workloads -- config 1 at 6,144 chains per GPU, configs 3, 4, 5 at 256 and config 5 at ONE chain per
 GPU (BASELINE's "8 independent chains across 8 GPUs" layout, the lane-group kernel) -- each with its own roofline where
 a PMC profile of that (config, chains, lanes) on this library build is committed (profiles/pmc_*.json), and its own
 CPU baseline with the reference-calibrated rate of that config (profiles/reference_timing_cfg<c>.json).
@@ -34,7 +34,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters
 VALU_PEAK = 1024 * 2.4e9 / 2   # wave64 VALU instructions/s: 1024 SIMDs, 2.4 GHz, one wave64 instruction per 2 cycles
 MODEL_NAMES = {"sir": "SIR", "seir": "SEIR", "sir_subgroups": "multi-subgroup SIR", "sir_subgroups2": "SIR subgroups2"}
 # the `configs` workloads: name -> (BASELINE config, chains per GPU)
-CONFIG_RUNS = {"1": (1, 3072, 3), "3": (3, 256, 1), "4": (4, 256, 1), "5": (5, 256, 1), "5x1": (5, 1, 1)}
+CONFIG_RUNS = {"1": (1, 6144, 4), "3": (3, 256, 1), "4": (4, 256, 1), "5": (5, 256, 1), "5x1": (5, 1, 1)}
 
 
 def parse():
@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--pipelines", type=int, default=int(os.environ.get("EPIPF_BENCH_PIPELINES", 0)),
                     help="chain groups on their own engine + host thread, so each group's MH host work overlaps the "
                          "others' filters (epipf.pmcmc.run_pipelined); 0 = the headline on one lockstep sampler and each "
-                         "`configs` entry at its own (CONFIG_RUNS: config 1 in three groups, DESIGN.md §7)")
+                         "`configs` entry at its own (CONFIG_RUNS: config 1 in four groups, DESIGN.md §7)")
     ap.add_argument("--prefetch", type=int, default=16, help="filter slots per round of the speculative single chain")
     # ~40 rounds: a speculative round commits ~8 iterations at config 2; 60 iterations (6 rounds) moved the adaptive
     # width's figure by +-20% from run to run (profiles/r4y_prefetch_cfg5.txt), 200 still by ~+-7% (BENCH_r05)
@@ -453,6 +453,7 @@ def config_runs(ctx, args):
     """The `configs` object: short timed runs of the other BASELINE workloads on every rank (one rank per GPU; the
     config-5 one-chain entry is BASELINE's 8-chain layout at 8 GPUs), at the config's own proposal and at
     fixed_theta where that differs."""
+    from epipf.engine import release_engines
     names = [] if args.configs.strip().lower() in ("", "none") else [c.strip() for c in args.configs.split(",")]
     out = {}
     cpu_done = {}
@@ -460,12 +461,15 @@ def config_runs(ctx, args):
         if name not in CONFIG_RUNS:
             raise SystemExit(f"bench.py: unknown --configs entry {name!r}")
         cfg, chains, pipes = CONFIG_RUNS[name]
+        release_engines()                                              # no idle contexts beside this entry's
+        gc.collect()
         steps = args.configs_steps * (5 if chains == 1 else 1)        # one-chain MH iterations are short
         from epipf import datasets
         Yc, mc = datasets.benchmark_dataset(cfg)
-        # config 1 (N x T = 5,000 per filter): one-workgroup filters (one per chain, 1024 to a launch) and the host
-        # draws in C, three chain groups on host threads so that each group's host work overlaps the others' filters
-        # (run_pipelined; profiles/r5v_cfg1_chains.jsonl: 256 chains 2.0e9, 1024 5.3e9, 3072 in three groups 1.2e10)
+        # config 1 (N x T = 5,000 per filter): one-workgroup filters (one per chain, 1,536 to a launch) and the host
+        # draws in C, four chain groups on host threads so that each group's host work overlaps the others' filters
+        # (run_pipelined; profiles/r5v_cfg1_chains.jsonl: 256 chains 2.0e9, 1024 5.3e9, 6144 in four groups
+        # 1.4-1.6e10; more groups than the 4 hardware queues share queues and stall)
         pipelines = (args.pipelines or pipes) if chains > 1 and mc["N"] * Yc.shape[0] <= 20000 else 1
         if cfg == 1:
             steps *= 10                                                # 2-3 ms MH steps: time a few hundred ms
@@ -581,7 +585,7 @@ def main():
         with np.errstate(divide="ignore", invalid="ignore"):
             rhat = [None if not np.isfinite(v) else float(v) for v in gelman_rubin(list(th_g))]
 
-    single = prefetch = None
+    single = prefetch = s1 = None
     if args.single_chain and rank == 0 and world == 1:
         from epipf.pmcmc import ChainSampler, chain_key
         s1 = ChainSampler(Y, meta["model"], list(meta["theta"]), run["h"], sigma=run["sigma"], iters=args.steps + 2,
@@ -601,6 +605,7 @@ def main():
         prefetch = prefetch_chain(args, Y, meta, N, T, local, args.prefetch, args.prefetch_iters, h=run["h"],
                                   sigma=run["sigma"], start=prefetch_auto["start_iteration"])
 
+    run["samplers"] = run["engines"] = s1 = None                       # the headline's contexts, released
     configs = config_runs(ctx, args)
 
     base = None

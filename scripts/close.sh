@@ -1,6 +1,6 @@
 #!/bin/bash
 # Closing measurement of a build: rocprofv3 trace + PMC passes (scripts/profile.sh) of every workload the bench line
-# reports -- the headline (config 2, 256 chains -> profiles/pmc_step_kernel.json), config 1 at 3,072 chains in three host
+# reports -- the headline (config 2, 256 chains -> profiles/pmc_step_kernel.json), config 1 at 6,144 chains in four host
 # pipelines (pmc_fused_cfg1.json: the one-workgroup filter), configs 3, 4, 5 at 256 chains
 # (pmc_step_cfg{3,4,5}.json) and config 5 at one chain per GPU (pmc_group_cfg5_c1.json) -- each
 # recording the library's build id, so the bench line's rooflines are those of the library it times; then the default
@@ -19,8 +19,8 @@ prof() {  # prof <tag> <json name> <env...>
     cp gpurun_out/prof_${T}_$tag/$name gpurun_out/$T/
 }
 has c2 && prof c2 pmc_step_kernel.json PMC_CONFIG=2 PMC_CHAINS=256
-has c1 && prof c1 pmc_fused_cfg1.json PMC_CONFIG=1 PMC_CHAINS=3072 PMC_LANES=1 PMC_KERNEL=pf_filter_wg_kernel \
-  EPIPF_FUSED=1 BENCH_ARGS="--config 1 --chains 3072 --pipelines 3" STEPS=20
+has c1 && prof c1 pmc_fused_cfg1.json PMC_CONFIG=1 PMC_CHAINS=6144 PMC_LANES=1 PMC_KERNEL=pf_filter_wg_kernel \
+  EPIPF_FUSED=1 BENCH_ARGS="--config 1 --chains 6144 --pipelines 4" STEPS=20
 for cfg in 3 4 5; do
   has c$cfg && prof c${cfg}x256 pmc_step_cfg$cfg.json PMC_CONFIG=$cfg PMC_CHAINS=256 BENCH_ARGS="--config $cfg"
 done

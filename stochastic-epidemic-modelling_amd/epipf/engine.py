@@ -272,6 +272,13 @@ class Engine:
 _CACHE = {}
 
 
+def release_engines():
+    """Drop the cached engines: each context closes (its device buffers and HIP streams freed) with its last
+    reference.  Idle contexts' streams still hold hardware queues (GPU_MAX_HW_QUEUES, 4 by default), on which the next
+    concurrently running engines may otherwise be placed together."""
+    _CACHE.clear()
+
+
 def get_engine(type_model, groups, n_particles, T, chains=1, device=0):
     """Cached engine large enough for (T, chains).  When a bigger one is needed a new context replaces the cached
     one; the old context is not closed here -- a sampler may still hold it -- but released with its last reference
