@@ -241,7 +241,7 @@ def timed_chains(ctx, args, cfg, chains, steps, warmup, kind, pipelines=1, strea
     between barriers (+ the end-of-run RCCL all-gather of the draws), then one untimed iteration with the device
     counters on.  Returns a dict of what the bench line reports."""
     from epipf import _lib, datasets
-    from epipf.distributed import gather_draws, pack_draws, shard
+    from epipf.distributed import gather_draws, shard
     from epipf.engine import Engine
     from epipf.pmcmc import ChainSampler, chain_key, run_pipelined
     Y, meta = datasets.benchmark_dataset(cfg)
@@ -290,8 +290,8 @@ def timed_chains(ctx, args, cfg, chains, steps, warmup, kind, pipelines=1, strea
     else:
         filters = sum(samplers[0].step() for _ in range(steps))
     # end of run: gather every rank's posterior draws over RCCL (xGMI), SURVEY.md §8e
-    results = [r for s_ in samplers for r in s_.results()]
-    gathered = gather_draws(pack_draws(results, upto=samplers[0].i), ctx.local, force=ctx.force_dist)
+    packed = np.concatenate([s_.packed_draws(upto=samplers[0].i) for s_ in samplers])   # == pack_draws(results())
+    gathered = gather_draws(packed, ctx.local, force=ctx.force_dist)
     ctx.barrier()
     dt = time.perf_counter() - t0
     a1, f1 = accept_counts()

@@ -56,12 +56,16 @@ def gather_draws(draws, device=0, force=False):
 
 def pack_draws(results, upto=None):
     """[C, iters*d + iters] rows of (thetas flattened, log-likelihoods) from ChainResult objects."""
-    rows = []
-    for r in results:
-        th = r.thetas if upto is None else r.thetas[:upto]
-        ll = r.log_likelihoods if upto is None else r.log_likelihoods[:upto]
-        rows.append(np.concatenate([th.reshape(-1), ll]))
-    return np.stack(rows)
+    if not results:
+        return np.stack([])                                   # numpy's own error for no chains, as before
+    n = len(results[0].log_likelihoods) if upto is None else min(int(upto), len(results[0].log_likelihoods))
+    d = results[0].thetas.shape[1]
+    out = np.empty((len(results), n * d + n))
+    th_out, ll_out = out[:, :n * d].reshape(-1, n, d), out[:, n * d:]
+    for k, r in enumerate(results):                           # one row per chain, written in place
+        th_out[k] = r.thetas[:n]
+        ll_out[k] = r.log_likelihoods[:n]
+    return out
 
 
 def unpack_draws(packed, d):

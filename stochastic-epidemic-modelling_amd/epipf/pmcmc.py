@@ -692,6 +692,12 @@ class ChainSampler:
         return [ChainResult(self.thetas[c], self.likelihoods[c], self.loglik[c], self.trajs[c],
                             int(self.acceptances[c]), int(self.filters_run[c])) for c in range(self.nc)]
 
+    def packed_draws(self, upto=None):
+        """epipf.distributed.pack_draws(self.results(), upto) for all chains at once: [chains, n d + n] rows of
+        (thetas flattened, log-likelihoods), n = upto or every iteration."""
+        n = self.iters if upto is None else min(int(upto), self.iters)
+        return np.concatenate([self.thetas[:, :n].reshape(self.nc, -1), self.loglik[:, :n]], axis=1)
+
 
 PIPELINE_SWITCH_S = 1e-4
 

@@ -120,6 +120,11 @@ def test_pipelined_samplers_equal_one_lockstep_sampler(datasets_golden):
         assert a.acceptances == b.acceptances and a.filters_run == b.filters_run
     with pytest.raises(ValueError):
         pm.run_pipelined([parts[0], parts[0]], 1)
+    from epipf.distributed import pack_draws
+    for upto in (None, 3, whole.i):                   # bench.py's vectorised gather rows == pack_draws(results())
+        np.testing.assert_array_equal(whole.packed_draws(upto), pack_draws(whole.results(), upto=upto))
+        np.testing.assert_array_equal(np.concatenate([s.packed_draws(upto) for s in parts]),
+                                      pack_draws(got, upto=upto))
 
 
 def test_random_sample_is_legacy_uniform():
