@@ -472,7 +472,7 @@ def config_runs(ctx, args):
         # 1.4-1.6e10; more groups than the 4 hardware queues share queues and stall)
         pipelines = (args.pipelines or pipes) if chains > 1 and mc["N"] * Yc.shape[0] <= 20000 else 1
         if cfg == 1:
-            steps *= 10                                                # 2-3 ms MH steps: time a few hundred ms
+            steps *= 25                                                # 2-3 ms MH steps: time a few hundred ms
         entry = None
         # N <= 512 (config 1): the engine's first eight runs of a batch size time the one-workgroup filter against the
         # step launches (EPIPF_FUSED=auto, epipf_api.cpp): warm up past them
