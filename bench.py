@@ -68,6 +68,9 @@ def parse():
     # ~40 rounds: a speculative round commits ~8 iterations at config 2; 60 iterations (6 rounds) moved the adaptive
     # width's figure by +-20% from run to run (profiles/r4y_prefetch_cfg5.txt), 200 still by ~+-7% (BENCH_r05)
     ap.add_argument("--prefetch-iters", type=int, default=400, help="MH iterations timed for the speculative chain")
+    ap.add_argument("--detail", default=None,
+                    help="file for the full result (every diagnostic and `configs` entry); the printed line is the "
+                         "compact form and names this file.  Default gpurun_out/bench_detail_n<N>.json")
     return ap.parse_args()
 
 
@@ -145,6 +148,10 @@ def cpu_baseline(Y, meta, N, seconds, cfg):
     if cal:
         f1, fall = cal["factor_port_over_reference_1core"], cal["factor_port_over_reference_allcores"]
         base["reference_calibrated"] = {
+            # an ESTIMATE: the factor was measured on the build container's CPU, the port's rate here on the GPU box's;
+            # dividing one by the other assumes the port/reference ratio does not depend on the host
+            "estimate": "cross-host extrapolation (port rate on this host / port-over-reference factor measured on "
+                        "the build container)",
             "reference_1core_value": value1 / f1,
             "reference_allcores_value": value / fall,
             "factor_port_over_reference_1core": f1,
@@ -306,11 +313,13 @@ def timed_chains(ctx, args, cfg, chains, steps, warmup, kind, pipelines=1, strea
     cst = stats_sum()
     dt_max, filters_all = ctx.max_sum(dt, filters)
     lanes = int(engines[0].stats()["last_lanes"]) or 1
-    fused = int(engines[0].stats().get("last_fused", 0))
+    # the path every engine took on its last run: the roofline's launch arithmetic assumes one path for all of them
+    paths = sorted({(int(e.stats().get("last_fused", 0)), int(e.stats()["last_lanes"]) or 1) for e in engines})
+    fused = paths[0][0]
     if fused:                                      # one launch per filter batch, one stream per engine
         streams = P
     return dict(Y=Y, meta=meta, N=N, T=T, chains=chains, P=P, streams=streams, samplers=samplers, engines=engines,
-                fused=fused,
+                fused=fused, paths=paths,
                 dt=dt_max, filters=filters, filters_all=filters_all, value=filters_all * N * T / dt_max, st=st, cst=cst,
                 lanes=lanes, h=h, sigma=sigma, proposal=pdesc, gathered=gathered,
                 acceptance_rate=(a1 - a0) / max(1, f1 - f0), steps=steps, warmup=warmup)
@@ -385,7 +394,7 @@ def roofline(run, value):
            else "HIP events (launch to completion)",
            "frac_hip_event_span": live_gbs / HBM_PEAK_GBS, "chip_level_frac": chip_gbs / HBM_PEAK_GBS,
            "bytes_per_particle_step": bytes_per_unit, "traffic": traffic, "traffic_raw": traffic_raw}
-    return {"bound": "valu", "kernel": kernel_name(run),
+    out = {"bound": "valu", "kernel": kernel_name(run),
             "achieved": valu["achieved"] if valu else None, "peak": VALU_PEAK,
             "unit": "wave64 VALU instr/s", "frac": valu["achieved"] / VALU_PEAK if valu else None,
             "traffic": traffic, "valu_issue": valu, "hbm": hbm,
@@ -395,6 +404,17 @@ def roofline(run, value):
             # HIP-event figure above also counts the time a launch waits for CUs held by concurrent chain-group launches
             "rocprof_avg_launch_us": rocprof_us,
             "pmc_profile": {"path": pmc_path, "build_id": pmc.get("build_id")}}
+    paths = run.get("paths", [(run.get("fused", 0), lanes)])
+    if len(paths) > 1:
+        # engines on different paths (one-workgroup filter vs step launches, or different lanes): the summed launch
+        # times over the summed launches mix two kernels, so no per-launch figure is physical
+        out["valid"] = False
+        out["invalid_reason"] = f"engines took different paths (fused, lanes): {paths}"
+        for k in ("achieved", "frac", "traffic"):
+            out[k] = None
+    else:
+        out["valid"] = True
+    return out
 
 
 def kernel_name(run):
@@ -517,10 +537,84 @@ def config_runs(ctx, args):
             entry["speedup_vs_cpu_baseline"] = entry["value"] / cpu_done[name]["value"]
             rc = cpu_done[name].get("reference_calibrated")
             if rc:
-                entry["speedup_vs_reference_1core_calibrated"] = entry["value"] / rc["reference_1core_value"]
-                entry["speedup_vs_reference_allcores_calibrated"] = entry["value"] / rc["reference_allcores_value"]
+                entry["speedup_vs_reference_1core_estimated"] = entry["value"] / rc["reference_1core_value"]
+                entry["speedup_vs_reference_allcores_estimated"] = entry["value"] / rc["reference_allcores_value"]
         out[name] = entry
     return out
+
+
+# The driver parses the JSON line out of an 8 KB stdout tail (BENCH_r05: a 21.7 KB line was not parsed).  The line
+# carries the headline with its full roofline and CPU baseline and one compact row per `configs` entry; everything
+# else goes to the detail file the line names.
+LINE_LIMIT = 6000
+# headline keys dropped, in this order, if the line still exceeds LINE_LIMIT (the detail file keeps them all)
+OPTIONAL_KEYS = ("gathered_rhat", "rank_devices", "proposal", "data", "speedup_vs_reference_allcores_estimated",
+                 "speedup_vs_reference_1core_estimated", "speedup_vs_cpu_single_core", "events_per_s",
+                 "single_chain_value")
+
+
+def compact_config(e):
+    """One `configs` entry as a row of the printed line: rate, timing, layout, roofline fractions, CPU baseline."""
+    r = e.get("roofline") or {}
+    cb = e.get("cpu_baseline") or {}
+    return {"value": e.get("value"), "ms_per_step": e.get("ms_per_step"), "steps": e.get("steps"),
+            "chains_per_gpu": e.get("chains_per_gpu"), "lanes": e.get("lanes_per_particle"),
+            "roofline_frac": r.get("frac"), "roofline_valid": r.get("valid", True),
+            "hbm_frac": (r.get("hbm") or {}).get("frac"),
+            "cpu_baseline": cb.get("value"), "cpu_cores": cb.get("cores"),
+            "acceptance_rate": e.get("acceptance_rate")}
+
+
+def compact_cpu_baseline(base):
+    if not base:
+        return base
+    out = {k: base[k] for k in ("value", "unit", "cores", "kind", "sample") if k in base}
+    if "single_core" in base:
+        out["single_core_value"] = base["single_core"]["value"]
+    rc = base.get("reference_calibrated")
+    if rc:
+        out["reference_estimate"] = {k: rc[k] for k in ("reference_1core_value", "reference_allcores_value",
+                                                       "factor_port_over_reference_1core", "estimate") if k in rc}
+    return out
+
+
+def compact_line(full, detail_path):
+    """The printed line: `full` without the bulky diagnostics, `configs` as compact rows, `detail` naming the file
+    that holds `full`.  Never longer than LINE_LIMIT characters."""
+    keep = ("metric", "value", "unit", "n_gpus", "ranks", "steps", "warmup", "ms_per_step", "higher_is_better",
+            "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "events_per_s",
+            "lanes_per_particle", "library_build_id", "single_chain_value", "speedup_vs_cpu_baseline",
+            "speedup_vs_cpu_single_core", "speedup_vs_reference_1core_estimated",
+            "speedup_vs_reference_allcores_estimated", "proposal", "gathered_draws_shape", "gathered_rhat",
+            "rank_devices")
+    line = {k: full[k] for k in keep if k in full}
+    line["cpu_baseline"] = compact_cpu_baseline(full.get("cpu_baseline"))
+    line["configs"] = {k: compact_config(v) for k, v in (full.get("configs") or {}).items()}
+    line["detail"] = detail_path
+    for k in OPTIONAL_KEYS:
+        if len(json.dumps(line)) <= LINE_LIMIT:
+            break
+        line.pop(k, None)
+    if len(json.dumps(line)) > LINE_LIMIT:           # last resort: the rows' secondary fields
+        for row in line["configs"].values():
+            for k in ("acceptance_rate", "cpu_cores", "lanes", "roofline_valid"):
+                row.pop(k, None)
+    return line
+
+
+def write_detail(full, path):
+    """Write the full result (every field, every `configs` entry in full) as JSON; returns the path written, or None
+    when it cannot be written (the printed line still goes out)."""
+    if path is None:
+        path = os.path.join(REPO, "gpurun_out", f"bench_detail_n{full.get('n_gpus', 1)}.json")
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(full, f, indent=1)
+    except OSError as e:
+        print(f"bench.py: could not write the detail file {path}: {e}", file=sys.stderr)
+        return None
+    return os.path.relpath(path, REPO) if os.path.abspath(path).startswith(REPO) else path
 
 
 def main():
@@ -670,10 +764,11 @@ def main():
             line["speedup_vs_cpu_baseline"] = value / base["value"]
             line["speedup_vs_cpu_single_core"] = value / base["single_core"]["value"]
             if "reference_calibrated" in base:
-                line["speedup_vs_reference_1core_calibrated"] = value / base["reference_calibrated"]["reference_1core_value"]
-                line["speedup_vs_reference_allcores_calibrated"] = \
+                line["speedup_vs_reference_1core_estimated"] = value / base["reference_calibrated"]["reference_1core_value"]
+                line["speedup_vs_reference_allcores_estimated"] = \
                     value / base["reference_calibrated"]["reference_allcores_value"]
-        print(json.dumps(line), flush=True)
+        detail = write_detail(line, args.detail)
+        print(json.dumps(compact_line(line, detail)), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

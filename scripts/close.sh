@@ -29,9 +29,9 @@ has c5x1 && prof c5x1 pmc_group_cfg5_c1.json PMC_CONFIG=5 PMC_CHAINS=1 PMC_LANES
 if has bench; then
   echo "== bench ($(date +%T))"
   cp gpurun_out/$T/pmc_*.json profiles/ 2>/dev/null
-  timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/$T/bench.log 2>&1 || { tail -5 gpurun_out/$T/bench.log; exit 1; }
-  tail -1 gpurun_out/$T/bench.log | python3 -c "
-import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']
+  timeout -k 10 600 python bench.py --steps 20 --warmup 5 --detail gpurun_out/$T/bench_detail.json > gpurun_out/$T/bench.log 2>&1 || { tail -5 gpurun_out/$T/bench.log; exit 1; }
+  python3 -c "
+import json,sys; d=json.load(open('gpurun_out/$T/bench_detail.json')); r=d['roofline']
 print('headline', f\"{d['value']:.4e}\", 'frac', r['frac'], 'single', f\"{d['single_chain_value']:.3e}\", 'pf16', f\"{d['single_chain_prefetch']['value']:.3e}\", 'pfauto', f\"{d['single_chain_prefetch_auto']['value']:.3e}\")
 for k, e in d['configs'].items(): print(k, f\"{e['value']:.4e}\", 'frac', e['roofline']['frac'], 'lanes', e['lanes_per_particle'], 'fixed', f\"{e.get('fixed_theta', {}).get('value', 0):.3e}\", 'pf', (e.get('prefetch_auto') or {}).get('value'))"
 fi

@@ -1,5 +1,5 @@
 """A short PMCMC run on the debug library (libepipf_debug.so: roctx ranges per epipf_run and filter step), for a
-rocprofv3 --marker-trace capture (scripts/r3_roctx_trace.sh).  Config 2 data, 4 chains, N = 2000, 3 MH iterations."""
+rocprofv3 --marker-trace capture (scripts/roctx_trace.sh).  Config 2 data, 4 chains, N = 2000, 3 MH iterations."""
 import os
 import sys
 

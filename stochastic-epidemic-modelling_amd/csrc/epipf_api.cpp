@@ -13,6 +13,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -59,6 +60,11 @@ int default_wg(int N) {
     return 64;
 }
 }  // namespace
+
+namespace epipf {
+// the host MH draws (host_mh.cpp) report their argument errors through the same per-thread message
+int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+}  // namespace epipf
 
 struct epipf_ctx {
     int device = 0, model = 0, G = 1, C = 3, K = 3, N = 0, Tmax = 0, max_chains = 0, wg = 64, B = 0;
@@ -116,21 +122,13 @@ struct epipf_ctx {
     int lane_blocks = 1280;  // automatic choice: lane groups up to this many particle blocks per launch
     int group_block = 0;     // lane-group runs' particles per block: 0 = automatic (pick_block), 16 or 64 (EPIPF_GROUP_BLOCK)
     int xcd_map = 1;         // XCD-aware placement of the step launches' blocks (EPIPF_XCD_MAP=0: 2-D grid)
+    int group_lone = -1;     // lane-group runs' unbounded instance: -1 = by the launch's waves (pick_group_lone),
+                             // 0 / 1 = never / wherever it exists (EPIPF_GROUP_LONE)
     // one-workgroup filter for N <= kFusedMaxN when the lanes are automatic: -1 = measured per batch size (FusedTune),
     // 1 = always, 0 = never (EPIPF_FUSED)
     int fused = -1;
     int fused_lanes = 0;     // its SSA lanes per particle: 0 = automatic (pick_fused), EPIPF_FUSED_LANES = 1/2/4/8/16
-    // Which path is faster depends on the events per particle-step, which the host cannot see ahead: one workgroup per
-    // chain wins where a step is little work or many chains fill the chip (config 1, N = 100, 6 events: 3.1x at 256
-    // chains, 1.3x at one), the step launches where one chain's many events want more than one CU (N = 100 at config
-    // 2's 90 events: 2.2x the other way).  So a batch size's first runs time both (the filter's device span, HIP
-    // events; results identical either way) and the faster one stays.
-    struct FusedTune {
-        int runs = 0;
-        double best[2] = {1e300, 1e300};   // fastest timed run: [0] step launches, [1] one-workgroup filter
-        int choice = -1;
-    };
-    std::map<int, FusedTune> fused_tune;   // by n_chains
+    uint64_t y_hash = 0;     // FNV-1a of the observations (epipf_set_observations): part of the path choice's key
     double split_p = -1.0;   // probs of the cached hi/lo split of log p, log1p(-p) (chains usually share probs)
     double split[4] = {0, 0, 0, 0};
 };
@@ -171,6 +169,19 @@ static int pick_block(const epipf_ctx* c, int W) {
     return W >= 16 ? kGroupBlock : c->wg;
 }
 
+// The lane-group kernel's instance without the minimum-waves bound (epipf_group.hpp, group_lone_instance: subgroup
+// models, G >= 2, W >= 8) when the launch's waves all stay resident at the unbounded kernel's occupancy -- 3 waves per
+// SIMD at G = 2 (143 VGPRs), 2 at G = 3, 1 at G = 4 -- on the chip's 1024 SIMDs: BASELINE config 5's one chain of 10^4
+// particles at W = 16 is 2,500 waves (2.4 per SIMD).  Larger launches keep the bounded instance (more waves resident, a
+// few spills: +7% / +14% at two / four chains, profiles/README.md).
+static int pick_group_lone(const epipf_ctx* c, const StepArgs& a, int n_chains) {
+    if (a.lanes < 8 || c->model < EPIPF_SIR_SUBGROUPS || c->G < 2) return 0;
+    if (c->group_lone >= 0) return c->group_lone;
+    const long waves = (long)n_chains * a.B * ((long)a.wg * a.lanes / 64);
+    const long per_simd = c->G == 2 ? 3 : c->G == 3 ? 2 : 1;
+    return waves <= per_simd * 1024 ? 1 : 0;
+}
+
 // Lanes per particle of the one-workgroup filter (epipf_fused.hpp), or 0 when the run takes the step launches: N <=
 // kFusedMaxN with the lanes automatic (an explicit epipf_set_lanes / EPIPF_LANES keeps the step kernels it names) and
 // the chain's LDS within the default launch limit.  W: EPIPF_FUSED_LANES where its N W lanes fit one workgroup, else 1.
@@ -181,22 +192,72 @@ static int pick_fused(const epipf_ctx* c) {
     return W;
 }
 
-// EPIPF_FUSED=auto (the default): runs 0-7 of a batch size alternate the paths (fused first, each path's first run
-// untimed), then each path's fastest of three timed runs decides, the step launches only by a 15% margin (concurrent
-// contexts -- run_pipelined -- share the device while they time, which spreads both paths' times).  *timed: this run's wall time is recorded.
-static bool fused_decide(epipf_ctx* c, int n_chains, bool& timed) {
-    timed = false;
-    if (c->fused >= 0) return c->fused == 1;
-    epipf_ctx::FusedTune& t = c->fused_tune[n_chains];
-    if (t.choice >= 0) return t.choice == 1;
-    timed = t.runs >= 2;                                 // runs 0, 1: warm-up of each path
-    return (t.runs & 1) == 0;                            // even runs: fused
+// Which path is faster depends on the events per particle-step, which the host cannot see ahead: one workgroup per
+// chain wins where a step is little work or many chains fill the chip (config 1, N = 100, 6 events: 3.1x at 256
+// chains, 1.3x at one), the step launches where one chain's many events want more than one CU (N = 100 at config
+// 2's 90 events: 2.2x the other way).  So a workload's first runs time both (the filter's device span, HIP events;
+// results identical either way) and the faster one stays.
+//
+// The choice is PER PROCESS, keyed on the workload (device, model, observation model, N, T, chains per run, the
+// observations and the population), not per context: contexts that run concurrently on one GPU (run_pipelined's chain
+// groups) pool their timed runs into one decision and all take the same path.  Each context deciding alone from
+// timings taken while the others ran let them settle on different paths.  A new dataset, T or population
+// is a new key, so epipf_set_observations / epipf_set_population start a fresh choice.
+struct FusedKey {
+    int device, model, G, obs, N, T, n_chains;
+    uint64_t data;
+    bool operator<(const FusedKey& o) const {
+        if (device != o.device) return device < o.device;
+        if (model != o.model) return model < o.model;
+        if (G != o.G) return G < o.G;
+        if (obs != o.obs) return obs < o.obs;
+        if (N != o.N) return N < o.N;
+        if (T != o.T) return T < o.T;
+        if (n_chains != o.n_chains) return n_chains < o.n_chains;
+        return data < o.data;
+    }
+};
+struct FusedTune {
+    int issued = 0;                    // tuning runs handed out (they alternate the paths)
+    int runs = 0;                      // tuning runs recorded
+    double best[2] = {1e300, 1e300};   // fastest timed run: [0] step launches, [1] one-workgroup filter
+    int choice = -1;
+};
+static std::mutex g_tune_mu;
+static std::map<FusedKey, FusedTune> g_tune;
+
+static uint64_t fnv1a(uint64_t h, const void* p, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 0x100000001b3ull; }
+    return h;
 }
 
-static void fused_record(epipf_ctx* c, int n_chains, bool fused, double seconds) {
-    epipf_ctx::FusedTune& t = c->fused_tune[n_chains];
+static FusedKey fused_key(const epipf_ctx* c, int obs, int n_chains) {
+    const uint64_t h = fnv1a(c->y_hash, c->npop, sizeof(double) * c->G);
+    return FusedKey{c->device, c->model, c->G, obs, c->N, c->T, n_chains, fnv1a(h, c->mu, sizeof(double) * c->G)};
+}
+
+// EPIPF_FUSED=auto (the default): the first 8 runs of a workload in this process alternate the paths (fused first, each
+// path's first run untimed), then each path's fastest of three timed runs decides, the step launches only by a 15%
+// margin (concurrent contexts share the device while they time, which spreads both paths' times).  *timed: this run's
+// device span is recorded; *tuning: the choice is still open.
+static bool fused_decide(const epipf_ctx* c, int obs, int n_chains, bool& timed, bool& tuning) {
+    timed = tuning = false;
+    if (c->fused >= 0) return c->fused == 1;
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    FusedTune& t = g_tune[fused_key(c, obs, n_chains)];
+    if (t.choice >= 0) return t.choice == 1;
+    tuning = true;
+    const int r = t.issued++;
+    timed = r >= 2;                                      // runs 0, 1: warm-up of each path
+    return (r & 1) == 0;                                 // even runs: fused
+}
+
+static void fused_record(const epipf_ctx* c, int obs, int n_chains, bool fused, double seconds) {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    FusedTune& t = g_tune[fused_key(c, obs, n_chains)];
     t.best[fused ? 1 : 0] = std::min(t.best[fused ? 1 : 0], seconds);
-    if (++t.runs >= 8) t.choice = t.best[0] < 0.85 * t.best[1] ? 0 : 1;
+    if (++t.runs >= 8 && t.choice < 0) t.choice = t.best[0] < 0.85 * t.best[1] ? 0 : 1;
 }
 
 static hipError_t launch_fused_run(const StepArgs& a, const epipf_ctx* c, int obs, int n_chains, const FilterStreams& fs) {
@@ -339,6 +400,7 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
         if (b == 0 || b == kGroupBlock || b == 64) c->group_block = b;
     }
     if (const char* e = getenv("EPIPF_XCD_MAP")) c->xcd_map = atoi(e) != 0;
+    if (const char* e = getenv("EPIPF_GROUP_LONE")) c->group_lone = strcmp(e, "auto") == 0 ? -1 : atoi(e) != 0;
     if (const char* e = getenv("EPIPF_FUSED")) c->fused = strcmp(e, "auto") == 0 ? -1 : atoi(e) != 0;
     if (const char* e = getenv("EPIPF_FUSED_LANES")) {
         const int w = atoi(e);
@@ -418,6 +480,7 @@ int epipf_set_observations(epipf_ctx* c, const double* Y, int T, int K) {
     HIP_TRY(hipMemcpyAsync(c->Y, Y, sizeof(double) * (size_t)T * K, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->T = T;
+    c->y_hash = fnv1a(0xcbf29ce484222325ull ^ (uint64_t)T, Y, sizeof(double) * (size_t)T * K);
     c->have_Y = true;
     return EPIPF_OK;
 }
@@ -508,12 +571,12 @@ static int run_impl(epipf_ctx* c, int n_chains, const double* theta, int d, int 
 
     StepArgs a{};
     a.N = c->N; a.T = c->T; a.max_chains = c->max_chains;
-    bool tune_timed = false;
-    const int fusedW = pick_fused(c) && fused_decide(c, n_chains, tune_timed) ? pick_fused(c) : 0;
-    const bool tuning = pick_fused(c) && c->fused < 0 && c->fused_tune[n_chains].choice < 0;
+    bool tune_timed = false, tuning = false;
+    const int fusedW = pick_fused(c) && fused_decide(c, obs_model, n_chains, tune_timed, tuning) ? pick_fused(c) : 0;
     a.lanes = fusedW ? fusedW : pick_lanes(c, n_chains);
     a.wg = fusedW ? 64 : pick_block(c, a.lanes);
     a.B = (c->N + a.wg - 1) / a.wg;
+    a.group_lone = fusedW ? 0 : pick_group_lone(c, a, n_chains);
     a.resample_mode = resample_mode; a.count_events = c->profiling >= EPIPF_PROFILE_COUNTERS ? 1 : 0; a.lf_max = c->lf_max;
     a.hist_stride = c->hist_stride; a.anc_stride = c->anc_stride; a.wstride = c->wstride; a.bstride = c->bstride;
     // S blocks per prefix segment: 1 (every block sum in LDS) for lane-group runs on 16-particle blocks up to
@@ -592,7 +655,7 @@ static int run_impl(epipf_ctx* c, int n_chains, const double* theta, int d, int 
                     // enter it, as they would a wall clock)
         float ms = 0.f;
         HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[2]));
-        fused_record(c, n_chains, fusedW != 0, tune_timed ? (double)ms : 1e300);
+        fused_record(c, obs_model, n_chains, fusedW != 0, tune_timed ? (double)ms : 1e300);
     }
     if (chosen) memcpy(traj_out, c->h_traj, sizeof(int32_t) * (size_t)n_chains * c->T * c->C);
     memcpy(status_out, c->h_status, sizeof(int32_t) * n_chains);

@@ -42,8 +42,19 @@ namespace epipf {
 // 3 waves per SIMD, without it: two to four chains of 10^4 particles need 4.9-9.8 waves per SIMD; with the bound 128 VGPRs
 // and a few spills, +7% / +14% at two / four chains of config 5, unchanged at one), none for SIR / SEIR (-5-7% at four
 // chains with it; profiles/r5i_group_waves_ab.txt).
+// EPIPF_GROUP_MIN_WAVES (a build flag, `make spill`) forces one bound on every instance: a register budget low enough
+// to spill on purpose, for the spill-robustness test (tests/test_gpu_spill.py).
+#ifndef EPIPF_GROUP_MIN_WAVES_SUB
+#define EPIPF_GROUP_MIN_WAVES_SUB 4
+#endif
 template <int MODEL>
-constexpr int group_min_waves() { return MODEL >= kSubgroups ? 4 : 1; }
+constexpr int group_min_waves() {
+#ifdef EPIPF_GROUP_MIN_WAVES
+    return EPIPF_GROUP_MIN_WAVES;
+#else
+    return MODEL >= kSubgroups ? EPIPF_GROUP_MIN_WAVES_SUB : 1;
+#endif
+}
 
 // Value of lane I of this lane's group of W consecutive lanes: DPP moves (groups of W <= 16 lie inside one DPP row),
 // a swizzle for W = 8.
@@ -336,7 +347,7 @@ __device__ __forceinline__ double population_of(const F& s) {
 // Day recorder of the ABC trial (abc_kernels.hip): `days` is every event's clock in order, with the state before it.
 // The filter records nothing.
 // Phase timing (make phase -> lib/libepipf_phase.so, EPIPF_PHASE_TIMING): s_memtime at the phase fences of the chunk
-// loop, summed per lane group; the step kernel prints each sampled wave's totals (scripts/r3d_phase_report.py).
+// loop, summed per lane group; the step kernel prints each sampled wave's totals (scripts/phase_report.py).
 // Scheduling fences between the chunk's phases (EPIPF_GROUP_FENCES=0 lets the compiler move work across them)
 #ifndef EPIPF_GROUP_FENCES
 #define EPIPF_GROUP_FENCES 1
@@ -630,8 +641,8 @@ inline size_t group_lds_bytes_impl(int B, int S, int C, int W, int K, int PB) {
 // (a.wg; the weight layout -- block sums, in-block prefixes -- is then one of 16-particle blocks, built by the init
 // kernel the same way).  Wave 0's first PB lanes hold the block's particles in the scan/search/gather and store/weigh
 // phases; the block is PB W / 64 waves.
-template <int MODEL, int G, int OBS, int W, int K, int PB>
-__global__ __launch_bounds__(PB * W, group_min_waves<MODEL>()) void pf_step_group_kernel(StepArgs a, int p) {
+template <int MODEL, int G, int OBS, int W, int K, int PB, int MINW>
+__global__ __launch_bounds__(PB * W, MINW) void pf_step_group_kernel(StepArgs a, int p) {
     using Sh = Shape<MODEL, G>;
     constexpr int C = Sh::C;
     constexpr int PPW = 64 / W;                          // particles per wave
@@ -784,16 +795,43 @@ __global__ __launch_bounds__(PB * W, group_min_waves<MODEL>()) void pf_step_grou
 }
 
 // ------------------------------------------------------------------------------- launch table
-template <int MODEL, int G, int OBS, int W, int K>
-static void launch_group_t(const StepArgs& a, int p, dim3 grid, size_t lds, hipStream_t s) {
+// The subgroup models' lane-group kernels at G >= 2 need more registers than the 4-wave bound leaves them (G = 2:
+// 143 VGPRs unbounded, 128 + 13-20 spilled under the bound; G = 3: ~205 vs 128 + ~180 spilled; G = 4: ~260 vs 128 +
+// ~500 spilled).  The bound pays where a launch has more waves than the unbounded kernel keeps resident (two to four
+// chains of 10^4 particles); a launch with fewer -- BASELINE config 5's one chain per GPU -- gains nothing from it and
+// pays the spills' scratch traffic on every chunk (7.2 MB written per launch).  So W >= 8 instances of
+// those models (the widths small launches take, pick_lanes) also exist without the bound, and the host picks them by the
+// launch's wave count (epipf_api.cpp, group_lone_waves).  Not in the forced-spill build (EPIPF_GROUP_MIN_WAVES).
+template <int MODEL, int G, int W>
+constexpr bool group_lone_instance() {
+#ifdef EPIPF_GROUP_MIN_WAVES
+    return false;
+#else
+    return group_min_waves<MODEL>() > 1 && MODEL >= kSubgroups && G >= 2 && W >= 8;
+#endif
+}
+
+template <int MODEL, int G, int OBS, int W, int K, int MINW>
+static void launch_group_pb(const StepArgs& a, int p, dim3 grid, size_t lds, hipStream_t s) {
     if constexpr (W >= 8) {                              // 16-particle blocks (a.wg, pick_block): W >= 8 only
         if (a.wg == kGroupBlock) {
-            hipLaunchKernelGGL((pf_step_group_kernel<MODEL, G, OBS, W, K, kGroupBlock>), grid, dim3(kGroupBlock * W), lds,
-                               s, a, p);
+            hipLaunchKernelGGL((pf_step_group_kernel<MODEL, G, OBS, W, K, kGroupBlock, MINW>), grid,
+                               dim3(kGroupBlock * W), lds, s, a, p);
             return;
         }
     }
-    hipLaunchKernelGGL((pf_step_group_kernel<MODEL, G, OBS, W, K, 64>), grid, dim3(64 * W), lds, s, a, p);
+    hipLaunchKernelGGL((pf_step_group_kernel<MODEL, G, OBS, W, K, 64, MINW>), grid, dim3(64 * W), lds, s, a, p);
+}
+
+template <int MODEL, int G, int OBS, int W, int K>
+static void launch_group_t(const StepArgs& a, int p, dim3 grid, size_t lds, hipStream_t s) {
+    if constexpr (group_lone_instance<MODEL, G, W>()) {
+        if (a.group_lone) {
+            launch_group_pb<MODEL, G, OBS, W, K, 1>(a, p, grid, lds, s);
+            return;
+        }
+    }
+    launch_group_pb<MODEL, G, OBS, W, K, group_min_waves<MODEL>()>(a, p, grid, lds, s);
 }
 
 // (lanes per particle W, events per lane per chunk K) instantiated.  K = 2 (round 4, fixed-point pass) measured +4% at

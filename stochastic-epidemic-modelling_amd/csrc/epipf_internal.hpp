@@ -67,6 +67,8 @@ struct StepArgs {
     double npop[kMaxG], mu[kMaxG], emu[kMaxG];
     int kmax[kMaxG];
     int fused_y, fused_lf;        // one-workgroup filter: Y / the log n! table staged in LDS (epipf_fused.hpp)
+    int group_lone;               // lane-group kernel: 1 = its instance without the minimum-waves register bound
+                                  // (group_lone_instance, epipf_group.hpp), for launches too small to need the waves
 };
 
 struct PathArgs {

@@ -95,12 +95,17 @@ constexpr int kMaxD = 32;
 
 }  // namespace
 
+namespace epipf {
+int set_error(int code, const char* msg);   // epipf_api.cpp: epipf_last_error()'s message for this thread
+}
+
 extern "C" {
 
 int epipf_mh_propose(int n_chains, int d, void* const* mt_states, const double* factors, const double* means,
                      double* props_out, void* dgemv) {
     if (n_chains < 0 || d < 2 || d > kMaxD || (d & 1) || !mt_states || !factors || !means || !props_out || !dgemv)
-        return EPIPF_EINVAL;
+        return epipf::set_error(EPIPF_EINVAL, "epipf_mh_propose: n_chains < 0, d outside the even values 2..32, or a "
+                                              "NULL argument");
     const Dgemv gemv = reinterpret_cast<Dgemv>(dgemv);
     double z[kMaxD], y[kMaxD];
     for (int c = 0; c < n_chains; ++c) {
@@ -113,7 +118,8 @@ int epipf_mh_propose(int n_chains, int d, void* const* mt_states, const double* 
 }
 
 int epipf_mh_peek(int n, const int32_t* chains, void* const* mt_states, int n_particles, int32_t* chosen_out) {
-    if (n < 0 || n_particles < 1 || !chains || !mt_states || !chosen_out) return EPIPF_EINVAL;
+    if (n < 0 || n_particles < 1 || !chains || !mt_states || !chosen_out)
+        return epipf::set_error(EPIPF_EINVAL, "epipf_mh_peek: n < 0, n_particles < 1 or a NULL argument");
     const uint32_t rng = (uint32_t)(n_particles - 1);
     uint32_t mask = rng;
     mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
@@ -143,7 +149,7 @@ int epipf_mh_peek(int n, const int32_t* chains, void* const* mt_states, int n_pa
 int epipf_mh_decide(int n, const int32_t* chains, void* const* mt_states, int n_particles, const double* lz_new,
                     const double* lz_old, int32_t* chosen_out, int32_t* accept_out) {
     if (n < 0 || n_particles < 1 || !chains || !mt_states || !lz_new || !lz_old || !chosen_out || !accept_out)
-        return EPIPF_EINVAL;
+        return epipf::set_error(EPIPF_EINVAL, "epipf_mh_decide: n < 0, n_particles < 1 or a NULL argument");
     for (int i = 0; i < n; ++i) {
         const int c = chains[i];
         MTState* s = static_cast<MTState*>(mt_states[c]);

@@ -75,10 +75,13 @@ def load():
     # One HIP runtime per process: torch (device memory, streams, RCCL for the multi-GPU gather) ships its own
     # libamdhip64 / ROCr.  Loaded first, the library's HIP dependency resolves to that same runtime; loaded after
     # libepipf's, torch's second runtime finds no GPU ("No HIP GPUs are available", scripts/torch_after_epipf.py).
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # EPIPF_NO_TORCH_PRELOAD=1 skips it for callers that never touch torch.  A torch that fails to import for any reason
+    # (a ROCm library mismatch raises OSError / RuntimeError, not ImportError) leaves the library loadable on its own.
+    if os.environ.get("EPIPF_NO_TORCH_PRELOAD") != "1":
+        try:
+            import torch  # noqa: F401
+        except Exception:  # noqa: BLE001
+            pass
     L = ctypes.CDLL(LIB_PATH)
     P = ctypes.c_void_p
     i32, u32, u64, f64 = ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double

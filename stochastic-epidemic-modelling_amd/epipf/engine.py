@@ -79,7 +79,7 @@ class Engine:
         self._L = L
         self._Y = None
         self._pop = None
-        self.bound_to = None                             # the ChainSampler whose data is loaded (ChainSampler._bind)
+        self.bound_to = None                             # token of the ChainSampler whose data is loaded (_bind)
         self.T = 0
 
     # ------------------------------------------------------------------ lifecycle

@@ -379,11 +379,14 @@ class ChainSampler:
         """(Re)load this sampler's observations and population into its engine before a run: a cached engine is
         shared with every other sampler / particle_filter call of the same model, N and device (no-op when
         unchanged, engine.set_observations / set_population compare first)."""
-        if getattr(self.eng, "bound_to", None) is self:   # nothing re-uploaded the engine's data since this sampler's
+        # the engine holds this sampler's token, not the sampler: no sampler -> engine -> sampler cycle keeping a
+        # finished sampler's arrays and the engine's HIP context alive until a GC cycle
+        tok = self.__dict__.setdefault("_bind_token", object())
+        if getattr(self.eng, "bound_to", None) is tok:    # nothing re-uploaded the engine's data since this sampler's
             return
         self.eng.set_observations(self._Y)
         self.eng.set_population(self._npop, self._mus)
-        self.eng.bound_to = self
+        self.eng.bound_to = tok
 
     def _propose(self, c, mean):
         """rngs[c].multivariate_normal(mean, h * std[c]) (pmcmc.py:277, :330) with the SVD factor cached per chain."""

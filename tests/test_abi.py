@@ -91,3 +91,11 @@ def test_debug_library_exports_the_same_boundary():
     D.epipf_build_id.restype = ctypes.c_char_p
     from epipf import _lib
     assert D.epipf_build_id().decode() == makefile_build_id() + "-debug", "libepipf_debug.so is stale"
+
+
+@pytest.mark.gpu
+def test_build_ids_match_the_sources_where_the_library_runs():
+    """The same two checks in the GPU run (the CPU-only check never ran on the box that receives the
+    prebuilt libraries): libepipf.so and libepipf_debug.so carry the build id of the sources shipped beside them."""
+    test_build_id_matches_the_sources()
+    test_debug_library_exports_the_same_boundary()

@@ -1,0 +1,79 @@
+"""bench.py's printed JSON line stays parseable by the driver, which reads it from an 8 KB stdout tail
+(BENCH_r05's 21.7 KB line was not parsed).  The fixture is the full line round 5's bench printed
+(profiles/r5z_bench.log), the shape `main()` builds before compacting it."""
+import copy
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import bench  # noqa: E402
+
+FULL = os.path.join(REPO, "tests", "golden", "bench_line_r05_full.json")
+
+
+def _full():
+    return json.load(open(FULL))
+
+
+def test_compact_line_fits_the_drivers_tail_and_keeps_the_headline():
+    full = _full()
+    assert len(json.dumps(full)) > 8192            # the round-5 line the driver could not parse
+    line = bench.compact_line(full, "gpurun_out/bench_detail_n1.json")
+    s = json.dumps(line)
+    assert len(s) <= bench.LINE_LIMIT <= 8192 - 1024, len(s)
+    assert json.loads(s) == line
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "config", "roofline", "cpu_baseline"):
+        assert k in line, k
+    assert line["value"] == full["value"] and line["ms_per_step"] == full["ms_per_step"]
+    assert line["roofline"] == full["roofline"]                      # the headline roofline in full
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert line["cpu_baseline"][k] == full["cpu_baseline"][k]
+    assert line["detail"] == "gpurun_out/bench_detail_n1.json"
+
+
+def test_compact_line_has_one_row_per_config():
+    full = _full()
+    line = bench.compact_line(full, None)
+    assert set(line["configs"]) == set(full["configs"])
+    for name, row in line["configs"].items():
+        e = full["configs"][name]
+        assert row["value"] == e["value"] and row["ms_per_step"] == e["ms_per_step"] and row["steps"] == e["steps"]
+        assert row["chains_per_gpu"] == e["chains_per_gpu"]
+        assert row["roofline_frac"] == e["roofline"]["frac"]
+        assert row["hbm_frac"] == e["roofline"]["hbm"]["frac"]
+        assert row["cpu_baseline"] == e["cpu_baseline"]["value"]
+
+
+def test_compact_line_stays_under_the_limit_when_inflated():
+    """Long strings and many configs: optional keys go first, and the line never exceeds LINE_LIMIT."""
+    full = _full()
+    full["data"] = "x" * 3000
+    full["gathered_rhat"] = [1.0] * 200
+    for i in range(6):
+        full["configs"][f"extra{i}"] = copy.deepcopy(full["configs"]["5"])
+    line = bench.compact_line(full, "d.json")
+    assert len(json.dumps(line)) <= bench.LINE_LIMIT
+    assert line["roofline"] == full["roofline"] and line["value"] == full["value"]
+    assert len(line["configs"]) == len(full["configs"])
+
+
+def test_detail_file_holds_the_full_result(tmp_path):
+    full = _full()
+    p = bench.write_detail(full, str(tmp_path / "detail.json"))
+    assert json.load(open(p)) == full
+
+
+def test_roofline_is_marked_invalid_when_engines_disagree():
+    """engines on different paths make the summed launch arithmetic unphysical; the roofline says so."""
+    st = {"step_kernel_launches": 8, "step_kernel_ms": 8.0, "step_ms": 9.0, "step_launches": 8}
+    run = {"st": st, "meta": {"model": "sir", "n_population": 200}, "N": 100, "T": 50, "lanes": 1, "steps": 2, "filters": 16,
+           "streams": 4, "fused": 1, "dt": 0.01, "cfg": 1, "chains": 8, "paths": [(0, 1), (1, 1)]}
+    r = bench.roofline(run, 1e9)
+    assert r["valid"] is False and "different paths" in r["invalid_reason"]
+    assert r["frac"] is None and r["achieved"] is None
+    run["paths"] = [(1, 1)]
+    assert bench.roofline(run, 1e9)["valid"] is True

@@ -278,6 +278,42 @@ def test_automatic_choice_times_both_paths_with_identical_results(datasets_golde
             np.testing.assert_array_equal(x, y)
 
 
+def test_automatic_choice_is_shared_by_the_processes_contexts(datasets_golden, monkeypatch):
+    """The path choice is per process and per workload (concurrent contexts each timing alone settled on
+    different paths): a second context on the same workload takes the first one's decision from its first run, without
+    tuning; new observations are a new workload, so that context tunes again (fused first)."""
+    from epipf.engine import Engine
+    monkeypatch.setenv("EPIPF_FUSED", "auto")
+    c = _case(datasets_golden, "seir")
+    th = np.tile([4.0, 1.0, 1.0], (2, 1))
+
+    def engine(Y):
+        e = Engine("seir", 1, 91, Y.shape[0], 2)
+        e.set_observations(Y)
+        e.set_population(c["npop"], c["mu"])
+        return e
+
+    a, b = engine(c["Y"]), engine(c["Y"])
+    used_a = []
+    for _ in range(9):
+        a.run(th, [0.1] * 2, [1, 2], [5, 5])
+        used_a.append(a.stats()["last_fused"])
+    assert used_a[:8] == [1, 0, 1, 0, 1, 0, 1, 0]
+    choice = used_a[8]
+    for _ in range(3):
+        b.run(th, [0.1] * 2, [1, 2], [5, 5])
+        assert b.stats()["last_fused"] == choice
+    # one more row of observations (T - 1 rows: a different T and data): tuning starts again
+    b.set_observations(c["Y"][:-1])
+    used_b = []
+    for _ in range(2):
+        b.run(th, [0.1] * 2, [1, 2], [5, 5])
+        used_b.append(b.stats()["last_fused"])
+    assert used_b == [1, 0]
+    a.close()
+    b.close()
+
+
 def test_many_chain_host_draws_on_the_device_engine(datasets_golden, monkeypatch):
     """24 chains of the config-1 shape (N = 100: the one-workgroup filter) through ChainSampler with the C host draws
     (epipf_mh_propose / epipf_mh_decide) and with the Python loop: identical thetas, likelihoods, paths, counters and

@@ -144,6 +144,31 @@ def test_lane_groups_larger_subgroup_models_equal_one_lane(datasets_golden, G):
         np.testing.assert_array_equal(got[0], ref[0])
 
 
+@pytest.mark.parametrize("lone", ["0", "1"])
+@pytest.mark.parametrize("G", [2, 3, 4])
+def test_subgroup_lane_groups_with_and_without_the_waves_bound(datasets_golden, monkeypatch, G, lone):
+    """The subgroup models' W >= 8 lane-group kernels exist with the 4-waves register bound (spilling at G >= 2) and
+    without it (epipf_group.hpp group_lone_instance; the host takes the unbounded one for launches whose waves all stay
+    resident, EPIPF_GROUP_LONE forces either): both are the oracle's, bit for bit."""
+    monkeypatch.setenv("EPIPF_GROUP_LONE", lone)
+    if G == 2:
+        c = _case(datasets_golden, "sir_subgroups")
+    else:
+        rs = np.random.RandomState(G)
+        c = dict(Y=np.tile(datasets_golden["sub_binom"][:6, :3], (1, G)), theta=(rs.uniform(0.5, 3.0, (G, G)), 0.7),
+                 obs=False, probs=0.1, npop=np.full(G, 1500.0), mu=np.full(G, 15.0), G=G)
+    for lanes in (8, 16):
+        lz, st, hid, anc, used = _run("sir_subgroups", c, 450, 2, lanes, [71, 72], [1, 6])
+        assert used == lanes
+        for ch in range(2):
+            o = oracle.particle_filter(c["Y"], "sir_subgroups", c["theta"], False, 0.1, 450, c["npop"], c["mu"],
+                                       key=[71, 72][ch], filter_index=[1, 6][ch])
+            assert int(st[ch]) == o["status"] == 0
+            np.testing.assert_array_equal(hid[ch], o["hidden"])
+            np.testing.assert_array_equal(anc[ch], o["ancestry"])
+            np.testing.assert_allclose(lz[ch], o["log_zetas"], rtol=1e-12, atol=1e-9)
+
+
 @pytest.mark.parametrize("lanes", [2, 16])
 def test_lane_groups_extinct_starts_and_short_horizons(datasets_golden, lanes):
     """Populations that die out inside a chunk of W events (mu = 1: many particles start with one infected) and
