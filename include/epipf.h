@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define EPIPF_ABI_VERSION 9
+#define EPIPF_ABI_VERSION 8
 
 /* return codes */
 #define EPIPF_OK 0
@@ -229,11 +229,6 @@ int epipf_mh_propose(int n_chains, int d, void* const* mt_states, const double* 
                      double* props_out, void* dgemv);
 int epipf_mh_decide(int n, const int32_t* chains, void* const* mt_states, int n_particles, const double* lz_new,
                     const double* lz_old, int32_t* chosen_out, int32_t* accept_out);
-/* epipf_mh_keep_paths: the iteration's sampled-trajectory rows of ChainSampler's iteration-major store (pmcmc.py:395 /
- * :400 -- sampled_trajs[:, i] = the accepted chain's new path, else the previous iteration's): for c < n_chains,
- * row[c][0 .. row_len) = accepted[c] ? (double)paths[c][.] : prev[c][.].  One pass over the rows. */
-int epipf_mh_keep_paths(int n_chains, int row_len, const double* prev, const int32_t* paths, const int32_t* accepted,
-                        double* row);
 /* epipf_mh_peek: chosen_out[c] = the randint(0, n_particles) the next epipf_mh_decide draws for each listed chain,
  * read on a copy of its state (nothing consumed): the path sampler's picks for epipf_run_sampled, before the filter. */
 int epipf_mh_peek(int n, const int32_t* chains, void* const* mt_states, int n_particles, int32_t* chosen_out);

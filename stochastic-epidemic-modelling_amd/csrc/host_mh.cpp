@@ -162,19 +162,4 @@ int epipf_mh_decide(int n, const int32_t* chains, void* const* mt_states, int n_
     return EPIPF_OK;
 }
 
-int epipf_mh_keep_paths(int n_chains, int row_len, const double* prev, const int32_t* paths, const int32_t* accepted,
-                        double* row) {
-    if (n_chains < 0 || row_len < 0 || !prev || !paths || !accepted || !row)
-        return epipf::set_error(EPIPF_EINVAL, "epipf_mh_keep_paths: n_chains < 0, row_len < 0 or a NULL argument");
-    for (int c = 0; c < n_chains; ++c) {
-        const size_t o = (size_t)c * row_len;
-        if (accepted[c]) {
-            for (int k = 0; k < row_len; ++k) row[o + k] = (double)paths[o + k];      // the new sampled path
-        } else {
-            memcpy(row + o, prev + o, sizeof(double) * row_len);                     // the previous iteration's
-        }
-    }
-    return EPIPF_OK;
-}
-
 }  // extern "C"

@@ -16,11 +16,11 @@ SIR, SEIR, SIR_SUBGROUPS, SIR_SUBGROUPS2 = 0, 1, 2, 3
 OBS_BINOMIAL, OBS_NORMAL = 0, 1
 RESAMPLE_MULTINOMIAL, RESAMPLE_SYSTEMATIC = 0, 1
 PROFILE_OFF, PROFILE_TIMING, PROFILE_COUNTERS = 0, 1, 2
-ABI_VERSION = 9
+ABI_VERSION = 8
 
 EXPORTS = (
     "epipf_create", "epipf_destroy", "epipf_set_observations", "epipf_set_population", "epipf_run",
-    "epipf_run_sampled", "epipf_mh_propose", "epipf_mh_decide", "epipf_mh_peek", "epipf_mh_keep_paths",
+    "epipf_run_sampled", "epipf_mh_propose", "epipf_mh_decide", "epipf_mh_peek",
     "epipf_copy_history", "epipf_path_sample", "epipf_simulate", "epipf_resample", "epipf_set_profiling",
     "epipf_get_stats", "epipf_reset_stats", "epipf_set_streams", "epipf_set_lanes", "epipf_last_error", "epipf_abi_version", "epipf_device_count",
     "epipf_build_id",
@@ -95,7 +95,6 @@ def load():
         "epipf_mh_propose": ([i32, i32, P, P, P, P, P], i32),
         "epipf_mh_decide": ([i32, P, P, i32, P, P, P, P], i32),
         "epipf_mh_peek": ([i32, P, P, i32, P], i32),
-        "epipf_mh_keep_paths": ([i32, i32, P, P, P, P], i32),
         "epipf_copy_history": ([P, i32, P, P], i32),
         "epipf_path_sample": ([P, i32, P, P], i32),
         "epipf_simulate": ([P, i32, P, P, i32, f64, u64, u32, u32, P, P], i32),

@@ -333,15 +333,10 @@ class ChainSampler:
         self.thetas = np.zeros((nc, self.iters, d))
         self.likelihoods = np.zeros((nc, self.iters))
         self.loglik = np.zeros((nc, self.iters))
-        # sampled trajectories, iteration-major over all chains ([iters][chains][T][C]: an MH iteration's rows of every
-        # chain are one contiguous block, so its bookkeeping is one block copy of the previous iteration plus the
-        # accepted chains' new paths -- per-chain fancy-indexed copies of [T, C] rows cost 1-3 ms an iteration at
-        # config 1's 1,536 chains per group); `trajs` is the [chains, T, iters, C] view of the reference layout
-        # Written through at allocation: np.zeros maps lazily zeroed pages, and the first touch of each iteration's
-        # 1.8 MB of rows (1,536 chains x T = 50 x C = 3) then cost ~2 ms of page faults inside the MH iteration.
-        self._tr = np.empty((self.iters, nc, T, Cc))
-        self._tr.fill(0.0)
-        self.trajs = self._tr.transpose(1, 2, 0, 3)
+        # sampled trajectories, iteration-major per chain (one contiguous [T, C] block per MH iteration, so an
+        # iteration's bookkeeping is a block copy); `trajs` is the [chains, T, iters, C] view of the reference layout
+        self._tr = np.zeros((nc, self.iters, T, Cc))
+        self.trajs = self._tr.transpose(0, 2, 1, 3)
         S = None if sigma is None else np.asarray(sigma, dtype=np.float64)
         if S is not None and S.ndim == 3 and S.shape[0] != nc:
             raise ValueError(f"sigma has {S.shape[0]} per-chain matrices for {nc} chains")
@@ -441,7 +436,7 @@ class ChainSampler:
         self.thetas[c, i] = self.thetas[c, i - 1]
         self.likelihoods[c, i] = self.likelihoods[c, i - 1]
         self.loglik[c, i] = self.loglik[c, i - 1]
-        self._tr[i, c] = self._tr[i - 1, c]
+        self._tr[c, i] = self._tr[c, i - 1]
 
     def initialise(self):
         """The initial draw loop, pmcmc.py:276-318 (repeat until theta >= 0 and the filter succeeded)."""
@@ -532,12 +527,12 @@ class ChainSampler:
                     self.thetas[0, i] = new
                     self.loglik[0, i] = lzT
                     self.likelihoods[0, i] = np.exp(out[0][0, -1])
-                    self._tr[i, 0] = tr
+                    self._tr[0, i] = tr
         if not take:                                              # rejected, negative or degenerate: previous row
             self.thetas[0, i] = self.thetas[0, i - 1]
             self.likelihoods[0, i] = self.likelihoods[0, i - 1]
             self.loglik[0, i] = self.loglik[0, i - 1]
-            self._tr[i, 0] = self._tr[i - 1, 0]
+            self._tr[0, i] = self._tr[0, i - 1]
         self.i += 1
         return ran
 
@@ -579,7 +574,6 @@ class ChainSampler:
         live = ~(P < 0).any(axis=1)                               # sum(prop < 0) > 0: no filter, :333-337
         lv = np.flatnonzero(live)
         acc = np.zeros(0, dtype=np.intp)
-        take_tr = None                                            # (accepted chains, their new paths [nc, T, C])
         if lv.size:
             if self.probs is None:                                # pmcmc.py:339-346: the last entry is probs
                 th_all, pr_all = P[:, :-1], np.clip(P[:, -1], 0.0, 1.0)
@@ -630,7 +624,7 @@ class ChainSampler:
                     self.thetas[acc, i] = new_all[acc]
                     self.loglik[acc, i] = lzT[acc]
                     self.likelihoods[acc, i] = np.exp(lzT[acc])
-                    take_tr = (acc, tr)
+                    self._tr[acc, i] = tr[acc]
             elif ok.size:
                 okl = ok.tolist()
                 if pre is None:
@@ -665,7 +659,7 @@ class ChainSampler:
                     self.thetas[acc, i] = new_all[acc]
                     self.loglik[acc, i] = lzT[acc]
                     self.likelihoods[acc, i] = np.exp(lzT[acc])
-                    take_tr = (acc, tr)
+                    self._tr[acc, i] = tr[acc]
         rej = np.ones(nc, dtype=bool)
         rej[acc] = False
         if rej.any():                                             # rejected, negative or degenerate: previous row
@@ -673,18 +667,7 @@ class ChainSampler:
             self.thetas[r, i] = self.thetas[r, i - 1]
             self.likelihoods[r, i] = self.likelihoods[r, i - 1]
             self.loglik[r, i] = self.loglik[r, i - 1]
-        # the iteration's trajectory rows: the accepted chains' new paths, every other chain's previous row -- in C
-        # with the C host draws (one pass), else two numpy passes
-        row = self._tr[i]
-        if take_tr is not None and self._host is not None:
-            paths = np.ascontiguousarray(take_tr[1], dtype=np.int32)
-            keep = (~rej).astype(np.int32)
-            _lib.check(_lib.load().epipf_mh_keep_paths(nc, row[0].size, _lib.ptr(self._tr[i - 1]), _lib.ptr(paths),
-                                                       _lib.ptr(keep), _lib.ptr(row)), "epipf_mh_keep_paths")
-        else:
-            row[...] = self._tr[i - 1]
-            if take_tr is not None:
-                np.copyto(row, take_tr[1], where=~rej[:, None, None])
+            self._tr[r, i] = self._tr[r, i - 1]
         self.i += 1
         return int(lv.size)
 
