@@ -5,7 +5,7 @@
 # (pmc_step_cfg{3,4,5}.json) and config 5 at one chain per GPU (pmc_group_cfg5_c1.json) -- each
 # recording the library's build id, so the bench line's rooflines are those of the library it times; then the default
 # bench line and the ABC bench.  Each step has its own time limit; a failure ends the script.
-#   TAG=r5z bash scripts/close.sh            (WHAT="c2 c1 c3 c4 c5 c5x1 bench abc" selects steps)
+#   TAG=r6z bash scripts/close.sh            (WHAT="c2 c1 c3 c4 c5 c5x1 bench rccl abc" selects steps)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -21,9 +21,12 @@ prof() {  # prof <tag> <json name> <env...>
 has c2 && prof c2 pmc_step_kernel.json PMC_CONFIG=2 PMC_CHAINS=256
 has c1 && prof c1 pmc_fused_cfg1.json PMC_CONFIG=1 PMC_CHAINS=6144 PMC_LANES=1 PMC_KERNEL=pf_filter_wg_kernel \
   EPIPF_FUSED=1 BENCH_ARGS="--config 1 --chains 6144 --pipelines 4" STEPS=20
-for cfg in 3 4 5; do
+for cfg in 3 4; do
   has c$cfg && prof c${cfg}x256 pmc_step_cfg$cfg.json PMC_CONFIG=$cfg PMC_CHAINS=256 BENCH_ARGS="--config $cfg"
 done
+# config 5 at h = 1: the initial-draw loop runs many launches with a handful of pending chains; ten timed iterations
+# keep the steady-state launches the larger share of the pass
+has c5 && prof c5x256 pmc_step_cfg5.json PMC_CONFIG=5 PMC_CHAINS=256 BENCH_ARGS="--config 5" STEPS=10
 has c5x1 && prof c5x1 pmc_group_cfg5_c1.json PMC_CONFIG=5 PMC_CHAINS=1 PMC_LANES=16 PMC_KERNEL=pf_step_group_kernel \
   BENCH_ARGS="--config 5 --chains 1" STEPS=20
 if has bench; then
@@ -34,6 +37,11 @@ if has bench; then
 import json,sys; d=json.load(open('gpurun_out/$T/bench_detail.json')); r=d['roofline']
 print('headline', f\"{d['value']:.4e}\", 'frac', r['frac'], 'single', f\"{d['single_chain_value']:.3e}\", 'pf16', f\"{d['single_chain_prefetch']['value']:.3e}\", 'pfauto', f\"{d['single_chain_prefetch_auto']['value']:.3e}\")
 for k, e in d['configs'].items(): print(k, f\"{e['value']:.4e}\", 'frac', e['roofline']['frac'], 'lanes', e['lanes_per_particle'], 'fixed', f\"{e.get('fixed_theta', {}).get('value', 0):.3e}\", 'pf', (e.get('prefetch_auto') or {}).get('value'))"
+fi
+if has rccl; then
+  echo "== rccl rehearsal ($(date +%T))"
+  CH=64 bash scripts/rccl_bench_check.sh > gpurun_out/$T/rccl.txt 2>&1 || { tail -5 gpurun_out/$T/rccl.txt; exit 1; }
+  cp gpurun_out/rccl_bench.log gpurun_out/$T/rccl_bench.log
 fi
 if has abc; then
   echo "== abc bench ($(date +%T))"

@@ -1,6 +1,6 @@
 """bench.py's printed JSON line stays parseable by the driver, which reads it from an 8 KB stdout tail
 (BENCH_r05's 21.7 KB line was not parsed).  The fixture is the full line round 5's bench printed
-(profiles/r5z_bench.log), the shape `main()` builds before compacting it."""
+(profiles/r5z_bench.log, in the history at commit 76ba74e), the shape `main()` builds before compacting it."""
 import copy
 import json
 import os
