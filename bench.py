@@ -382,13 +382,15 @@ def roofline(run, value):
         # older ones: the launch average over the grid's particle-steps
         per_ps = pmc.get("valu_per_particle_step") or (ins / units if ins and units else None)
         if per_ps:
-            busy = pmc.get("valu_busy_frac")
+            # over the MH iterations' dispatches alone where the pass recorded it (PMC_TIMED_DISPATCHES)
+            busy = pmc.get("valu_busy_frac_timed") or pmc.get("valu_busy_frac")
             valu = {"achieved": per_ps * value, "instr_per_particle_step": per_ps,
                     "cycles_per_instr_at_2.4GHz": VALU_PEAK * 2 / (per_ps * value),
                     # VALU pipe busy per SIMD-cycle, SQ_ACTIVE_INST_VALU / GRBM_GUI_ACTIVE of the PMC pass: the
                     # cycle-weighted utilisation (each instruction weighted by the cycles it holds the pipe -- f64,
                     # transcendental and 64-bit-product instructions more than the flat peak's 2)
                     "pmc_valu_busy_frac": busy,
+                    "pmc_busy_over": "MH iterations' dispatches" if pmc.get("valu_busy_frac_timed") else "all dispatches",
                     # the flat peak prices every wave64 instruction at 2 cycles (VALU_PEAK)
                     "flat_peak": VALU_PEAK, "flat_frac": per_ps * value / VALU_PEAK,
                     # the issue rate this instruction mix would reach with the pipe always busy

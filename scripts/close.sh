@@ -21,12 +21,13 @@ prof() {  # prof <tag> <json name> <env...>
 has c2 && prof c2 pmc_step_kernel.json PMC_CONFIG=2 PMC_CHAINS=256
 has c1 && prof c1 pmc_fused_cfg1.json PMC_CONFIG=1 PMC_CHAINS=6144 PMC_LANES=1 PMC_KERNEL=pf_filter_wg_kernel \
   EPIPF_FUSED=1 BENCH_ARGS="--config 1 --chains 6144 --pipelines 4" STEPS=20
-for cfg in 3 4; do
-  has c$cfg && prof c${cfg}x256 pmc_step_cfg$cfg.json PMC_CONFIG=$cfg PMC_CHAINS=256 BENCH_ARGS="--config $cfg"
-done
-# config 5 at h = 1: the initial-draw loop runs many launches with a handful of pending chains; ten timed iterations
-# keep the steady-state launches the larger share of the pass
-has c5 && prof c5x256 pmc_step_cfg5.json PMC_CONFIG=5 PMC_CHAINS=256 BENCH_ARGS="--config 5" STEPS=10
+has c3 && prof c3x256 pmc_step_cfg3.json PMC_CONFIG=3 PMC_CHAINS=256 BENCH_ARGS="--config 3"
+# configs 4 and 5 propose at h = 5 / h = 1: their initial-draw loops run many launches with a handful of pending chains,
+# so the busy fraction is also taken over the MH iterations' launches alone (the last (steps + 2) x (T - 1) x 4
+# dispatches: warm-up, timed and counters iterations, four chain-group streams; PMC_TIMED_DISPATCHES)
+has c4 && prof c4x256 pmc_step_cfg4.json PMC_CONFIG=4 PMC_CHAINS=256 BENCH_ARGS="--config 4" PMC_TIMED_DISPATCHES=$(((3 + 2) * 14 * 4))
+has c5 && prof c5x256 pmc_step_cfg5.json PMC_CONFIG=5 PMC_CHAINS=256 BENCH_ARGS="--config 5" STEPS=10 \
+  PMC_TIMED_DISPATCHES=$(((10 + 2) * 13 * 4))
 has c5x1 && prof c5x1 pmc_group_cfg5_c1.json PMC_CONFIG=5 PMC_CHAINS=1 PMC_LANES=16 PMC_KERNEL=pf_step_group_kernel \
   BENCH_ARGS="--config 5 --chains 1" STEPS=20
 if has bench; then

@@ -88,6 +88,12 @@ def main(d):
     both = [k for k in act if k in gui]
     if both:
         out["valu_busy_frac"] = 4.0 * sum(act[k] for k in both) / (1024.0 * sum(gui[k] for k in both) / 8.0)
+        # PMC_TIMED_DISPATCHES = D: the same fraction over the pass's last D dispatches -- the bench run's MH iterations
+        # after its initial-draw loop (at h = 1 that loop's launches carry a handful of live chains each)
+        if TIMED and len(both) > TIMED:
+            last = sorted(both, key=lambda k: int(k[1]))[-TIMED:]
+            out["valu_busy_frac_timed"] = 4.0 * sum(act[k] for k in last) / (1024.0 * sum(gui[k] for k in last) / 8.0)
+            out["timed_dispatches"] = TIMED
     lanes = float(meta.get("Grid_Size") or 0) / LANES
     if lanes > 0:   # LANES lanes per particle (padding of the last block included: < 0.5% at N = 10^4)
         out["particle_steps_per_launch"] = lanes
@@ -108,6 +114,7 @@ CHAINS = int(os.environ["PMC_CHAINS"]) if os.environ.get("PMC_CHAINS") else None
 KERNEL = os.environ.get("PMC_KERNEL", "pf_step_kernel")                                  # kernel name profiled
 LANES = int(os.environ.get("PMC_LANES", "1"))                                            # its lanes per particle
 NAME = os.environ.get("PMC_NAME", "pmc_step_kernel.json")
+TIMED = int(os.environ.get("PMC_TIMED_DISPATCHES", "0"))                                 # last D dispatches: timed
 
 if __name__ == "__main__":
     main(sys.argv[1])
