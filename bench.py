@@ -347,6 +347,24 @@ def pmc_profile(cfg, chains, lanes):
     return {}, None
 
 
+def loop_ceiling(cfg):
+    """The SSA event loop's measured ceiling for this config on the library timed here (profiles/loop_ceiling.json,
+    scripts/loop_ceiling.sh: the library's own event loop with every lane busy, eight waves per SIMD; matched on build
+    id like the PMC passes).  Returns (entry, path) or ({}, None)."""
+    from epipf import _lib
+    path = os.path.join(REPO, "profiles", "loop_ceiling.json")
+    try:
+        p = json.load(open(path))
+    except (OSError, ValueError):
+        return {}, None
+    c = p.get("configs", {}).get(str(cfg)) or {}
+    if p.get("build_id") != _lib.build_id() or "uniform" not in c:
+        return {}, None
+    e = dict(c["uniform"])
+    e["lane_events_per_s_distinct"] = (c.get("distinct") or {}).get("lane_events_per_s")
+    return e, os.path.relpath(path, REPO)
+
+
 def roofline(run, value):
     """Roofline of the run's dominant kernel: pf_step_kernel (one lane per particle) or pf_step_group_kernel (W lanes
     per particle).  Both are bound by vector-instruction issue (the SSA event loop), not by HBM: the
@@ -385,16 +403,21 @@ def roofline(run, value):
             # over the MH iterations' dispatches alone where the pass recorded it (PMC_TIMED_DISPATCHES)
             busy = pmc.get("valu_busy_frac_timed") or pmc.get("valu_busy_frac")
             valu = {"achieved": per_ps * value, "instr_per_particle_step": per_ps,
-                    "cycles_per_instr_at_2.4GHz": VALU_PEAK * 2 / (per_ps * value),
-                    # VALU pipe busy per SIMD-cycle, SQ_ACTIVE_INST_VALU / GRBM_GUI_ACTIVE of the PMC pass: the
-                    # cycle-weighted utilisation (each instruction weighted by the cycles it holds the pipe -- f64,
-                    # transcendental and 64-bit-product instructions more than the flat peak's 2)
-                    "pmc_valu_busy_frac": busy,
-                    "pmc_busy_over": "MH iterations' dispatches" if pmc.get("valu_busy_frac_timed") else "all dispatches",
                     # the flat peak prices every wave64 instruction at 2 cycles (VALU_PEAK)
                     "flat_peak": VALU_PEAK, "flat_frac": per_ps * value / VALU_PEAK,
-                    # the issue rate this instruction mix would reach with the pipe always busy
-                    "cycle_weighted_peak": per_ps * value / busy if busy else None}
+                    # AMD's VALUBusy (SQ_ACTIVE_INST_VALU / GRBM_GUI_ACTIVE) of the PMC pass: per-wave VALU cycles
+                    # per SIMD-cycle, ~1.1 at the loop's ceiling (dual issue), and the pass serialises the chain
+                    # groups' dispatches, so it reads low against the live run
+                    "pmc_valu_busy_frac": busy,
+                    "pmc_busy_over": "MH iterations' dispatches" if pmc.get("valu_busy_frac_timed") else "all dispatches"}
+    ceil, ceil_path = loop_ceiling(run["cfg"])
+    cst = run.get("cst") or {}
+    ev_ps = cst["events"] / cst["particle_steps"] if cst.get("particle_steps") else None
+    if valu and ceil:
+        # the loop's own saturated issue rate (PMC pass of the ceiling run): achieved / ceiling near 1 = the SIMDs
+        # issue VALU as fast as the loop can; the events fraction below is what that issue buys (lane use, phases)
+        valu["ceiling"] = ceil["valu_instr_per_s"]
+        valu["issue_frac"] = valu["achieved"] / ceil["valu_instr_per_s"]
     hbm_us = rocprof_us or avg_launch_s * 1e6
     hbm_gbs = units_per_launch * bytes_per_unit / (hbm_us / 1e6) / 1e9
     hbm = {"achieved": hbm_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_gbs / HBM_PEAK_GBS,
@@ -402,14 +425,20 @@ def roofline(run, value):
            else "HIP events (launch to completion)",
            "frac_hip_event_span": live_gbs / HBM_PEAK_GBS, "chip_level_frac": chip_gbs / HBM_PEAK_GBS,
            "bytes_per_particle_step": bytes_per_unit, "traffic": traffic, "traffic_raw": traffic_raw}
-    # frac: the cycle-weighted VALU utilisation (PMC busy fraction; VERDICT r5: the flat 2-cycle peak misprices the
-    # loop's f64 / transcendental / 64-bit-product instructions), against the mix's own attainable issue rate
-    cw = valu and valu.get("cycle_weighted_peak")
-    out = {"bound": "valu", "kernel": kernel_name(run),
-            "achieved": valu["achieved"] if valu else None, "peak": cw if cw else VALU_PEAK,
-            "peak_kind": "cycle-weighted (achieved / PMC VALU busy fraction)" if cw else "flat (2 cycles per wave64 instr)",
-            "unit": "wave64 VALU instr/s",
-            "frac": (valu["pmc_valu_busy_frac"] if cw else valu["achieved"] / VALU_PEAK) if valu else None,
+    # frac: SSA events (the path's algorithmic unit, every particle's events) per second against the measured ceiling
+    # of the same event loop on this chip -- every lane busy, no per-step phases, no launch tails, eight waves per SIMD
+    # (scripts/loop_ceiling.hip).  Without a ceiling of this build: VALU issue against the flat 2-cycle peak.
+    if ceil and ev_ps:
+        prim = {"achieved": value * ev_ps, "peak": ceil["lane_events_per_s"], "unit": "lane-events/s",
+                "peak_kind": f"measured SSA-loop ceiling, every lane busy ({ceil_path})",
+                "frac": value * ev_ps / ceil["lane_events_per_s"],
+                "events_per_particle_step": ev_ps,
+                "ceiling_one_particle_per_lane": ceil.get("lane_events_per_s_distinct")}
+    else:
+        prim = {"achieved": valu["achieved"] if valu else None, "peak": VALU_PEAK, "unit": "wave64 VALU instr/s",
+                "peak_kind": "flat (2 cycles per wave64 instr)",
+                "frac": valu["achieved"] / VALU_PEAK if valu else None}
+    out = {"bound": "valu", "kernel": kernel_name(run), **prim,
             "traffic": traffic, "valu_issue": valu, "hbm": hbm,
             "avg_launch_us": avg_launch_s * 1e6, "particle_steps_per_launch": units_per_launch,
             "concurrent_launches_per_step": run["streams"], "step_wall_us": step_wall_s * 1e6,

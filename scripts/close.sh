@@ -3,14 +3,15 @@
 # reports -- the headline (config 2, 256 chains -> profiles/pmc_step_kernel.json), config 1 at 6,144 chains in four host
 # pipelines (pmc_fused_cfg1.json: the one-workgroup filter), configs 3, 4, 5 at 256 chains
 # (pmc_step_cfg{3,4,5}.json) and config 5 at one chain per GPU (pmc_group_cfg5_c1.json) -- each
-# recording the library's build id, so the bench line's rooflines are those of the library it times; then the default
-# bench line and the ABC bench.  Each step has its own time limit; a failure ends the script.
-#   TAG=r6z bash scripts/close.sh            (WHAT="c2 c1 c3 c4 c5 c5x1 bench rccl abc" selects steps)
+# recording the library's build id, so the bench line's rooflines are those of the library it times; the SSA loop's
+# ceiling (scripts/loop_ceiling.sh -> loop_ceiling.json, the rooflines' peak); then the default bench line and the ABC
+# bench.  Each step has its own time limit; a failure ends the script.
+#   TAG=r6z bash scripts/close.sh            (WHAT="c2 c1 c3 c4 c5 c5x1 ceiling bench rccl abc" selects steps)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 T=${TAG:-close}
-WHAT=${WHAT:-c2 c1 c3 c4 c5 c5x1 bench abc}
+WHAT=${WHAT:-c2 c1 c3 c4 c5 c5x1 ceiling bench abc}
 mkdir -p gpurun_out/$T
 has() { [[ " $WHAT " == *" $1 "* ]]; }
 prof() {  # prof <tag> <json name> <env...>
@@ -30,13 +31,18 @@ has c5 && prof c5x256 pmc_step_cfg5.json PMC_CONFIG=5 PMC_CHAINS=256 BENCH_ARGS=
   PMC_TIMED_DISPATCHES=$(((10 + 2) * 13 * 4))
 has c5x1 && prof c5x1 pmc_group_cfg5_c1.json PMC_CONFIG=5 PMC_CHAINS=1 PMC_LANES=16 PMC_KERNEL=pf_step_group_kernel \
   BENCH_ARGS="--config 5 --chains 1" STEPS=20
+if has ceiling; then
+  echo "== loop ceiling ($(date +%T))"
+  bash scripts/loop_ceiling.sh > gpurun_out/$T/ceiling.log 2>&1 || { tail -5 gpurun_out/$T/ceiling.log; exit 1; }
+  cp gpurun_out/ceiling/loop_ceiling.json gpurun_out/$T/ && cp gpurun_out/ceiling/loop_ceiling.json profiles/
+fi
 if has bench; then
   echo "== bench ($(date +%T))"
   cp gpurun_out/$T/pmc_*.json profiles/ 2>/dev/null
   timeout -k 10 600 python bench.py --steps 20 --warmup 5 --detail gpurun_out/$T/bench_detail.json > gpurun_out/$T/bench.log 2>&1 || { tail -5 gpurun_out/$T/bench.log; exit 1; }
   python3 -c "
 import json,sys; d=json.load(open('gpurun_out/$T/bench_detail.json')); r=d['roofline']
-print('headline', f\"{d['value']:.4e}\", 'frac', r['frac'], 'single', f\"{d['single_chain_value']:.3e}\", 'pf16', f\"{d['single_chain_prefetch']['value']:.3e}\", 'pfauto', f\"{d['single_chain_prefetch_auto']['value']:.3e}\")
+print('headline', f\"{d['value']:.4e}\", 'frac', r['frac'], 'issue', (r.get('valu_issue') or {}).get('issue_frac'), 'single', f\"{d['single_chain_value']:.3e}\", 'pf16', f\"{d['single_chain_prefetch']['value']:.3e}\", 'pfauto', f\"{d['single_chain_prefetch_auto']['value']:.3e}\")
 for k, e in d['configs'].items(): print(k, f\"{e['value']:.4e}\", 'frac', e['roofline']['frac'], 'lanes', e['lanes_per_particle'], 'fixed', f\"{e.get('fixed_theta', {}).get('value', 0):.3e}\", 'pf', (e.get('prefetch_auto') or {}).get('value'))"
 fi
 if has rccl; then

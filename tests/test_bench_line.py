@@ -77,3 +77,28 @@ def test_roofline_is_marked_invalid_when_engines_disagree():
     assert r["frac"] is None and r["achieved"] is None
     run["paths"] = [(1, 1)]
     assert bench.roofline(run, 1e9)["valid"] is True
+
+
+def test_roofline_peak_is_the_measured_loop_ceiling(monkeypatch):
+    """The VALU roofline's peak is the SSA loop's measured ceiling (profiles/loop_ceiling.json) when it was taken on
+    the library timed here, in lane-events/s; otherwise the flat VALU issue peak."""
+    st = {"step_kernel_launches": 8, "step_kernel_ms": 8.0, "step_ms": 9.0, "step_launches": 8}
+    run = {"st": st, "meta": {"model": "sir", "n_population": 10000}, "N": 10000, "T": 200, "lanes": 1, "steps": 2,
+           "filters": 16, "streams": 4, "dt": 0.01, "cfg": 2, "chains": 8,
+           "cst": {"events": 9.0e9, "particle_steps": 1.0e8}}
+    ceil = {"lane_events_per_s": 6.0e11, "valu_instr_per_s": 6.3e11, "lane_events_per_s_distinct": 5.0e11}
+    monkeypatch.setattr(bench, "loop_ceiling", lambda cfg: (ceil, "profiles/loop_ceiling.json"))
+    r = bench.roofline(run, 5.0e9)
+    assert r["unit"] == "lane-events/s" and r["peak"] == 6.0e11
+    assert abs(r["achieved"] - 5.0e9 * 90.0) < 1.0 and abs(r["frac"] - 0.75) < 1e-12
+    monkeypatch.setattr(bench, "loop_ceiling", lambda cfg: ({}, None))
+    r = bench.roofline(run, 5.0e9)
+    assert r["peak"] == bench.VALU_PEAK and r["peak_kind"].startswith("flat")
+
+
+def test_committed_loop_ceiling_has_every_config():
+    """profiles/loop_ceiling.json (scripts/loop_ceiling.sh) covers every BASELINE config the bench line reports."""
+    d = json.load(open(os.path.join(REPO, "profiles", "loop_ceiling.json")))
+    for c in ("1", "2", "3", "4", "5"):
+        assert d["configs"][c]["uniform"]["lane_events_per_s"] > d["configs"][c]["distinct"]["lane_events_per_s"] > 0
+    assert len(d["build_id"]) == 16
