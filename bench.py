@@ -372,6 +372,9 @@ def roofline(run, value):
     the HBM figures the north star asks for are in `hbm` (algorithmic 8C + 40 B per particle-step over the launch
     duration)."""
     st, meta, N = run["st"], run["meta"], run["N"]
+    # one GPU's roofline: this rank's share of the whole-job rate (`value` counts every rank's filters; N > 1 ranks)
+    if run.get("filters_all"):
+        value = value * run["filters"] / run["filters_all"]
     lanes = run["lanes"]
     steps = run["steps"]
     launches = max(1, st["step_kernel_launches"])

@@ -102,3 +102,15 @@ def test_committed_loop_ceiling_has_every_config():
     for c in ("1", "2", "3", "4", "5"):
         assert d["configs"][c]["uniform"]["lane_events_per_s"] > d["configs"][c]["distinct"]["lane_events_per_s"] > 0
     assert len(d["build_id"]) == 16
+
+
+def test_roofline_is_one_gpus_share_of_the_job(monkeypatch):
+    """At N > 1 ranks `value` is the whole job's rate; the roofline divides it down to this rank's filters."""
+    st = {"step_kernel_launches": 8, "step_kernel_ms": 8.0, "step_ms": 9.0, "step_launches": 8}
+    run = {"st": st, "meta": {"model": "sir", "n_population": 10000}, "N": 10000, "T": 200, "lanes": 1, "steps": 2,
+           "filters": 16, "filters_all": 128, "streams": 4, "dt": 0.01, "cfg": 2, "chains": 8,
+           "cst": {"events": 9.0e9, "particle_steps": 1.0e8}}
+    ceil = {"lane_events_per_s": 6.0e11, "valu_instr_per_s": 6.3e11}
+    monkeypatch.setattr(bench, "loop_ceiling", lambda cfg: (ceil, "profiles/loop_ceiling.json"))
+    r = bench.roofline(run, 8 * 5.0e9)
+    assert abs(r["frac"] - 0.75) < 1e-12
