@@ -54,7 +54,6 @@ def main():
         e["valu_busy"] = 4.0 * best["SQ_ACTIVE_INST_VALU"] / (1024.0 * cyc)
         e["valu_dual_issue_frac"] = 4.0 * best["SQ_ACTIVE_INST_VALU2"] / (1024.0 * cyc)
         e["clock_ghz"] = cyc / best["dur"] / 1e9
-        e["pmc_lane_events_per_s_note"] = "PMC run's dispatches are timed by the profiler; lane_events_per_s is the HIP-event figure"
         out["configs"].setdefault(str(e["config"]), {})[e["variant"]] = e
     print(json.dumps(out, indent=1))
 
