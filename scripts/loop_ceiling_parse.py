@@ -44,7 +44,9 @@ def main():
     # the PMC run repeats the natural run: per (config, variant) one warm-up launch and three timed launches
     assert len(disp) == 4 * len(natural), (len(disp), len(natural))
     out = {"build_id": build_id(), "source": "scripts/loop_ceiling.hip (fast_propagate of csrc/epipf_device.hpp)",
-           "unit": "lane-events/s (SSA events, every lane counted)", "configs": {}}
+           "unit": "lane-events/s (SSA events, every lane counted)",
+           "note": "lane_events_per_s: HIP events around each launch (best of three); valu_instr_per_s, valu_busy, "
+                   "clock_ghz: the rocprofv3 PMC run of the same launches", "configs": {}}
     for i, e in enumerate(natural):
         timed = disp[4 * i + 1:4 * i + 4]
         best = max(timed, key=lambda t: t["SQ_INSTS_VALU"] / t["dur"])
