@@ -114,3 +114,31 @@ def test_roofline_is_one_gpus_share_of_the_job(monkeypatch):
     monkeypatch.setattr(bench, "loop_ceiling", lambda cfg: (ceil, "profiles/loop_ceiling.json"))
     r = bench.roofline(run, 8 * 5.0e9)
     assert abs(r["frac"] - 0.75) < 1e-12
+
+
+def test_loop_ceiling_parse_reads_the_runs(tmp_path):
+    """scripts/loop_ceiling_parse.py: per (config, variant) the HIP-event rate of the plain run and, from the PMC
+    run's counter CSV (one warm-up and three timed launches each), wave64 VALU instr/s and VALU busy of the best."""
+    import csv
+    import subprocess
+    lines = [{"config": 2, "variant": v, "lane_events_per_s": r, "ms": 1.0, "events_per_call": 90.0, "waves": 8192,
+              "calls_per_lane": 1, "waves_per_simd_cap": 0} for v, r in (("uniform", 6.0e11), ("distinct", 5.0e11))]
+    (tmp_path / "natural.jsonl").write_text("".join(json.dumps(x) + "\n" for x in lines))
+    (tmp_path / "pmc").mkdir()
+    with open(tmp_path / "pmc" / "run_counter_collection.csv", "w", newline="") as fh:
+        w = csv.DictWriter(fh, fieldnames=["Dispatch_Id", "Counter_Name", "Counter_Value", "Start_Timestamp",
+                                           "End_Timestamp"])
+        w.writeheader()
+        for d in range(8):
+            dur_ns = 1_000_000                                         # 1 ms per launch
+            for name, v in (("SQ_INSTS_VALU", 6.0e8 + d), ("SQ_ACTIVE_INST_VALU", 6.0e8),
+                            ("SQ_ACTIVE_INST_VALU2", 1.0e8), ("GRBM_GUI_ACTIVE", 8 * 2.4e6)):
+                w.writerow({"Dispatch_Id": d + 1, "Counter_Name": name, "Counter_Value": v,
+                            "Start_Timestamp": 10_000_000 * d, "End_Timestamp": 10_000_000 * d + dur_ns})
+    out = subprocess.run([sys.executable, os.path.join(REPO, "scripts", "loop_ceiling_parse.py"), str(tmp_path)],
+                         capture_output=True, text=True, check=True).stdout
+    d = json.loads(out)
+    u = d["configs"]["2"]["uniform"]
+    assert u["lane_events_per_s"] == 6.0e11 and abs(u["valu_instr_per_s"] - (6.0e8 + 3) / 1e-3) < 1.0
+    assert abs(u["clock_ghz"] - 2.4) < 1e-9 and abs(u["valu_busy"] - 4 * 6.0e8 / (1024 * 2.4e6)) < 1e-9
+    assert d["configs"]["2"]["distinct"]["valu_instr_per_s"] == (6.0e8 + 7) / 1e-3
