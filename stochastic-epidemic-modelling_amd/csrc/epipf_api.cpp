@@ -122,9 +122,6 @@ struct epipf_ctx {
     int lane_blocks = 1280;  // automatic choice: lane groups up to this many particle blocks per launch
     int group_block = 0;     // lane-group runs' particles per block: 0 = automatic (pick_block), 16 or 64 (EPIPF_GROUP_BLOCK)
     int xcd_map = 1;         // XCD-aware placement of the step launches' blocks (EPIPF_XCD_MAP=0: 2-D grid)
-    int compact = 0;         // compacting step's stop threshold (EPIPF_COMPACT, live lanes per wave; 0 = off)
-    char* queue = nullptr;   // its particle queue (StepArgs::q*), allocated on first use
-    size_t queue_bytes = 0;
     int group_lone = -1;     // lane-group runs' unbounded instance: -1 = by the launch's waves (pick_group_lone),
                              // 0 / 1 = never / wherever it exists (EPIPF_GROUP_LONE)
     // one-workgroup filter for N <= kFusedMaxN when the lanes are automatic: -1 = measured per batch size (FusedTune),
@@ -314,7 +311,7 @@ static void free_ctx(epipf_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     void* dev[] = {c->hidden, c->ancestry, c->res, c->chosen, c->traj, c->wraw, c->wloc, c->bsum,
-                   c->Y, c->lf, c->cp, c->logtab, c->scratch, c->abc, c->queue};
+                   c->Y, c->lf, c->cp, c->logtab, c->scratch, c->abc};
     for (void* p : dev)
         if (p) (void)hipFree(p);
     void* host[] = {c->h_cp, c->h_res, c->h_traj};
@@ -403,7 +400,6 @@ int epipf_create(epipf_ctx** out, int device, int model, int groups, int n_parti
         if (b == 0 || b == kGroupBlock || b == 64) c->group_block = b;
     }
     if (const char* e = getenv("EPIPF_XCD_MAP")) c->xcd_map = atoi(e) != 0;
-    if (const char* e = getenv("EPIPF_COMPACT")) c->compact = std::max(0, std::min(63, atoi(e)));
     if (const char* e = getenv("EPIPF_GROUP_LONE")) c->group_lone = strcmp(e, "auto") == 0 ? -1 : atoi(e) != 0;
     if (const char* e = getenv("EPIPF_FUSED")) c->fused = strcmp(e, "auto") == 0 ? -1 : atoi(e) != 0;
     if (const char* e = getenv("EPIPF_FUSED_LANES")) {
@@ -601,27 +597,6 @@ static int run_impl(epipf_ctx* c, int n_chains, const double* theta, int d, int 
     a.counters = c->counters;
     a.lane_events = pick_lane_events(c, a.lanes);
     a.xcd_map = c->xcd_map;
-    a.compact = 0;
-    if (!fusedW && a.lanes == 1 && c->compact > 0) {   // the compacting step's queue: [max_chains][N] entries
-        const size_t n = (size_t)c->max_chains * c->N;
-        const size_t need = n * (sizeof(double) + sizeof(float) + 3 * sizeof(int32_t) + sizeof(int32_t) * (size_t)c->C)
-                            + sizeof(int32_t) * (size_t)c->max_chains;
-        if (need > c->queue_bytes) {
-            if (c->queue) { HIP_TRY(hipStreamSynchronize(c->stream)); (void)hipFree(c->queue); c->queue = nullptr; c->queue_bytes = 0; }
-            if (hipMalloc((void**)&c->queue, need) != hipSuccess) return fail(EPIPF_ENOMEM, "compaction queue hipMalloc(%zu) failed", need);
-            c->queue_bytes = need;
-            HIP_TRY(hipMemsetAsync(c->queue, 0, need, c->stream));
-        }
-        char* q = c->queue;
-        a.qrem = reinterpret_cast<double*>(q); q += n * sizeof(double);
-        a.qR = reinterpret_cast<float*>(q); q += n * sizeof(float);
-        a.qks = reinterpret_cast<uint32_t*>(q); q += n * sizeof(uint32_t);
-        a.qnev = reinterpret_cast<int32_t*>(q); q += n * sizeof(int32_t);
-        a.qj = reinterpret_cast<int32_t*>(q); q += n * sizeof(int32_t);
-        a.qx = reinterpret_cast<int32_t*>(q); q += n * c->C * sizeof(int32_t);
-        a.qcount = reinterpret_cast<int32_t*>(q);
-        a.compact = c->compact;
-    }
     if (a.lanes > 1 && !group_shape_supported(a.lanes, a.lane_events))
         return fail(EPIPF_EINVAL, "no lane-group kernel for %d lanes x %d events", a.lanes, a.lane_events);
     c->stats.last_lanes = a.lanes;

@@ -1008,130 +1008,6 @@ __device__ __forceinline__ bool fast_propagate(double* x, const ChainParam& cp, 
     return true;
 }
 
-// ------------------------------------------------------------------------------- compacting step (EPIPF_COMPACT)
-// The loop state of a particle whose wave stopped before it finished (pf_step_kernel<..., COMPACT>): the counts
-// reached (x), the remaining time in units of 1/ln 2, the clock's rate sum, the next event's counter word and the
-// events so far.  Every field is exactly what fast_propagate holds between two iterations, so a resumed particle
-// takes the same decisions bit for bit.
-struct FastResume {
-    double rem;
-    float R;
-    uint32_t ks;
-    int nev;
-};
-constexpr int kFastDone = 1, kFastExact = 0, kFastStopped = 2;
-
-// fast_propagate's loop in two halves.  MODE 1 (the compacting step's first pass): every lane starts at event 0, the
-// counter word stays wave-uniform, and the whole wave stops at the top of an iteration once at most stop_thr of its
-// lanes are still running; those lanes return kFastStopped with x and rs holding their loop state.  MODE 2 (the
-// continuation, pf_resume_kernel): lanes resume queued particles from different events, so the counter word is
-// per lane (its Philox products leave the scalar unit).  Returns kFastDone (x final, nev_out events), kFastExact
-// (the exact path must redo the step: as fast_propagate returning false) or kFastStopped.
-template <int MODEL, int G, int MODE>
-__device__ __forceinline__ int fast_propagate_c(double* x, const ChainParam& cp, uint32_t j, uint32_t ptag,
-                                                double tmax, int& nev_out, int& iters, bool& eligible,
-                                                FastResume& rs, int stop_thr) {
-    using F = FastSsa<MODEL, G>;
-    constexpr int NCH = F::NCH;
-    iters = 0;
-    nev_out = 0;
-    eligible = false;
-    if (!(cp.flags & kChainFastSsa)) return kFastExact;
-    F st;
-    if (!st.load(x, cp)) return kFastExact;
-    eligible = true;
-    const float kB = F::kBand * cp.band_slack;
-    const float Bt = (float)(tmax * kInvLn2) * F::kClockT * cp.clock_slack;   // from the step's full length
-    double rem = tmax * kInvLn2;
-    float R = 0.f, df = 0.f, B = 0.f;
-    uint32_t ks = 0;
-    int nev0 = 0;
-    if constexpr (MODE == 2) {
-        rem = rs.rem;
-        R = rs.R;
-        ks = rs.ks;
-        nev0 = rs.nev;
-    }
-    bool alive = st.active(), ok = true;
-    int ch = 0;
-    constexpr int GD = NCH > 3 ? G : 1;
-    float dS[GD], dI[GD];
-    Block rn{0u, 0u, 0u, 0u};
-    if (alive) rn = philox<true>(ks, j, ptag, cp.f, cp.k0, cp.k1);
-    while (alive) {
-        if constexpr (MODE == 1) {
-            if (__builtin_popcountll(__ballot(1)) <= stop_thr) break;      // wave-uniform: the live lanes stop
-        }
-        const Block r = rn;
-        if constexpr (MODE == 2) ks = ks + 1u;
-        else ks = __builtin_amdgcn_readfirstlane(ks) + 1u;
-        rn = philox<true>(ks, j, ptag, cp.f, cp.k0, cp.k1);
-        float c[NCH - 1];
-        const float total = st.cum(c);
-        const float ri = __builtin_amdgcn_rcpf(total);
-        const float uc = __uint_as_float(0x3F800000u | (r.w >> 9)) - (1.0f - kUlpF);
-        uint64_t below[NCH - 1];
-        if constexpr (NCH <= 3) {
-            bool close = false;
-            ch = 0;
-#pragma unroll
-            for (int i = 0; i < NCH - 1; ++i) {
-                const float q = c[i] * ri;
-                ch += (q < uc) ? 1 : 0;
-                close |= fabsf(q - uc) <= kB;
-            }
-            if (close) ch = st.exact_channel(cp, u01(r.z, r.w));
-        } else {
-            const float Tlo = (uc - kB) * total, Thi = fmaf(2.0f * kB, total, Tlo);
-            uint64_t unsure = 0;
-#pragma unroll
-            for (int i = 0; i < NCH - 1; ++i) {
-                below[i] = __ballot(c[i] < Tlo);
-                unsure |= below[i] ^ __ballot(c[i] < Thi);
-            }
-            if (unsure) {
-                const bool mine = __builtin_amdgcn_inverse_ballot_w64(unsure);
-                int che = 0;
-                if (mine) che = st.exact_channel(cp, u01(r.z, r.w));
-#pragma unroll
-                for (int i = 0; i < NCH - 1; ++i) below[i] = (below[i] & ~unsure) | __ballot(mine && che > i);
-            }
-        }
-        const uint32_t nh = ~r.y;
-        float lg = __builtin_amdgcn_logf((float)nh * 0x1.0p-32f);
-        if (nh < 0x1000000u) {
-            if (nh < 4096u) lg = tiny_log2(~r.x, r.y);
-            else lg = __builtin_amdgcn_logf(fmaf((float)nh, 0x1.0p-32f, (float)r.x * 0x1.0p-64f));
-        }
-        rem = rem + (double)(lg * ri);
-        R += ri;
-        df = (float)rem;
-        B = fmaf(R, kClockRF, Bt);
-        ok = df > B;
-        if constexpr (NCH <= 3) st.apply(ch, 1.f);
-        else st.apply_below(below, dS, dI);
-        alive = ok && st.active();
-    }
-    if constexpr (MODE == 1) {
-        if (alive) {                                                   // stopped with its wave: the loop state
-            rs.nev = st.save(x);
-            rs.rem = rem;
-            rs.R = R;
-            rs.ks = ks;
-            return kFastStopped;
-        }
-    }
-    if (!ok) {
-        if (!(df < -B)) return kFastExact;
-        if constexpr (NCH <= 3) st.apply(ch, -1.f);
-        else st.undo(dS, dI);
-    }
-    const int nev = st.save(x);
-    nev_out = nev0 + nev;
-    iters = nev + (ok ? 0 : 1);
-    return kFastDone;
-}
-
 // The exact loop over [0, tmax] from the parent state x (every lane that enters starts at event 0 together, so
 // the event index k is wave-uniform).  Software pipelining: event k+1's Philox block (counter-based, so
 // independent of event k's outcome) is computed while event k's f64 work runs, which gives each wave two

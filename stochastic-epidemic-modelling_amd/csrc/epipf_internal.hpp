@@ -69,15 +69,6 @@ struct StepArgs {
     int fused_y, fused_lf;        // one-workgroup filter: Y / the log n! table staged in LDS (epipf_fused.hpp)
     int group_lone;               // lane-group kernel: 1 = its instance without the minimum-waves register bound
                                   // (group_lone_instance, epipf_group.hpp), for launches too small to need the waves
-    int compact;                  // > 0: compacting step (EPIPF_COMPACT): a wave's first pass stops once at most this
-                                  // many of its lanes still run; pf_resume_kernel continues the queued particles
-    int32_t* qcount;              // per chain: particles queued by the step's first pass (reset by pf_weight_kernel)
-    double* qrem;                 // the queue, [chain][N]: FastResume fields, particle index, counts (qx: [.][C])
-    float* qR;
-    uint32_t* qks;
-    int32_t* qnev;
-    int32_t* qj;
-    int32_t* qx;
 };
 
 struct PathArgs {

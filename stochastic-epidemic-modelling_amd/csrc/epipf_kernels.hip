@@ -66,10 +66,7 @@ __global__ __launch_bounds__(WG) void pf_init_kernel(StepArgs a) {
     }
 }
 
-// COMPACT (EPIPF_COMPACT): the first pass of a compacting step -- a wave stops its SSA loop once at
-// most a.compact of its lanes still run and queues those particles (pf_resume_kernel continues them 64 to a wave);
-// the weights and block scan then run in pf_weight_kernel, after every particle of the step is done.
-template <int MODEL, int G, int OBS, int WG, bool COMPACT = false>
+template <int MODEL, int G, int OBS, int WG>
 __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs a, int p) {
     using Sh = Shape<MODEL, G>;
     constexpr int C = Sh::C;
@@ -144,45 +141,16 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
 #pragma unroll
     for (int c = 0; c < C; ++c) x[c] = 0.0;
     const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
-    bool fast_ok = false, eligible = false, stopped = false;
-    FastResume rs{};
+    bool fast_ok = false, eligible = false;
     if (j < a.N) {
         anc = checked_index(anc, a.N);
         a.ancestry[(size_t)chain * a.anc_stride + (size_t)p * a.N + j] = anc;   // :193
         const int32_t* hp = a.hidden + (size_t)chain * a.hist_stride + ((size_t)(p - 1) * a.N + anc) * C;
 #pragma unroll
         for (int c = 0; c < C; ++c) x[c] = (double)hp[c];
-        if constexpr (COMPACT) {
-            const int res = fast_propagate_c<MODEL, G, 1>(x, cp, (uint32_t)j, ptag, 1.0, nev, iters, eligible, rs,
-                                                          a.compact);
-            fast_ok = res == kFastDone;
-            stopped = res == kFastStopped;
-        } else {
-            fast_ok = fast_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, nev, iters, eligible);
-        }
+        fast_ok = fast_propagate<MODEL, G>(x, cp, (uint32_t)j, ptag, 1.0, nev, iters, eligible);
     }
-    exact = (j < a.N && !fast_ok && !stopped) ? 1 : 0;
-    if constexpr (COMPACT) {   // the stopped lanes' loop states to the chain's queue (one atomic per wave)
-        const unsigned long long sm = __ballot(stopped);
-        if (sm) {
-            const int first = (int)__builtin_ctzll(sm);
-            int base = 0;
-            if (tid == first) base = atomicAdd(a.qcount + chain, (int)__popcll(sm));
-            base = __shfl(base, first, 64);
-            if (stopped) {
-                const size_t qi = (size_t)chain * a.N + base + (int)__popcll(sm & ((1ull << tid) - 1ull));
-                a.qj[qi] = j;
-#pragma unroll
-                for (int c = 0; c < C; ++c) a.qx[qi * C + c] = (int32_t)x[c];
-                a.qrem[qi] = rs.rem;
-                a.qR[qi] = rs.R;
-                a.qks[qi] = rs.ks;
-                a.qnev[qi] = rs.nev;
-                nev = rs.nev;
-                iters = rs.nev;
-            }
-        }
-    }
+    exact = (j < a.N && !fast_ok) ? 1 : 0;
     if (__any(exact != 0)) {
         for (int i = tid; i < kLogTabEntries; i += WG) tab[i] = a.logtab[i];
         __syncthreads();
@@ -216,14 +184,12 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
             }
         }
     }
-    if (j < a.N && !stopped) {
+    if (j < a.N) {
         int32_t* hc = a.hidden + (size_t)chain * a.hist_stride + ((size_t)p * a.N + j) * C;
 #pragma unroll
         for (int c = 0; c < C; ++c) hc[c] = (int32_t)x[c];                        // :222-231
         // (a) weights of the new state against Y[p], used by step p+1, :178-181
-        if constexpr (!COMPACT) {
-            if (p + 1 < a.T) w = particle_weight<MODEL, G, OBS>(x, a.Y + (size_t)p * Sh::K, cp, a.cp + chain, a.lf, a.lf_max, hc);
-        }
+        if (p + 1 < a.T) w = particle_weight<MODEL, G, OBS>(x, a.Y + (size_t)p * Sh::K, cp, a.cp + chain, a.lf, a.lf_max, hc);
     }
     if (a.count_events) {  // accepted events; lane-iterations; wave-iterations x 64 (lane utilisation)
         unsigned long long e = (unsigned long long)nev, li = (unsigned long long)iters;
@@ -243,133 +209,12 @@ __global__ __launch_bounds__(WG, EPIPF_STEP_WAVES) void pf_step_kernel(StepArgs 
             atomicAdd(slot + 5, ex ? 1ull : 0ull);                        // waves with at least one
         }
     }
-    if constexpr (!COMPACT) {
-        if (p + 1 < a.T) {
-            const double loc = block_inclusive_scan<WG>(w, red);
-            a.wraw[wcur + j] = w;
-            a.wloc[wcur + j] = loc;
-            if (tid == WG - 1) a.bsum[bcur + bp.b] = loc;
-        }
+    if (p + 1 < a.T) {
+        const double loc = block_inclusive_scan<WG>(w, red);
+        a.wraw[wcur + j] = w;
+        a.wloc[wcur + j] = loc;
+        if (tid == WG - 1) a.bsum[bcur + bp.b] = loc;
     }
-}
-
-// The compacting step's continuation: the particles pf_step_kernel<..., true> queued, 64 to a wave, resumed where
-// their waves stopped (per-lane counter words, fast_propagate_c MODE 2) and run to the end of the step; a lane the
-// f32 loop hands back at the step boundary is replayed exactly from its parent (coop_replay), as in the step kernel.
-// Grid: maxw blocks per chain of the launch's group; blocks past the chain's queue return at once.
-template <int MODEL, int G>
-__global__ __launch_bounds__(64) void pf_resume_kernel(StepArgs a, int p, int maxw) {
-    constexpr int C = Shape<MODEL, G>::C;
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    LogTab* tab = reinterpret_cast<LogTab*>(smem);
-    const int chain = a.chain0 + (int)blockIdx.x / maxw;
-    const int w = (int)blockIdx.x % maxw;
-    if (a.status[chain] != 0) return;
-    const int cnt = a.qcount[chain];
-    if (w * 64 >= cnt) return;
-    const int tid = threadIdx.x;
-    const int slot = w * 64 + tid;
-    const bool live = slot < cnt;
-    const ChainParam cp = a.cp[chain];
-    const size_t qi = (size_t)chain * a.N + slot;
-    double x[C];
-#pragma unroll
-    for (int c = 0; c < C; ++c) x[c] = 0.0;
-    int j = 0;
-    FastResume rs{};
-    if (live) {
-        j = checked_index(a.qj[qi], a.N);
-#pragma unroll
-        for (int c = 0; c < C; ++c) x[c] = (double)a.qx[qi * C + c];
-        rs.rem = a.qrem[qi];
-        rs.R = a.qR[qi];
-        rs.ks = a.qks[qi];
-        rs.nev = a.qnev[qi];
-    }
-    const uint32_t ptag = ((uint32_t)p & 0xFFFFFFu) | kDomainSSA;
-    int nev = 0, iters = 0, res = kFastDone;
-    bool eligible = false;
-    if (live) res = fast_propagate_c<MODEL, G, 2>(x, cp, (uint32_t)j, ptag, 1.0, nev, iters, eligible, rs, 0);
-    const bool exact = live && res != kFastDone;
-    if (__any(exact)) {
-        for (int i = tid; i < kLogTabEntries; i += 64) tab[i] = a.logtab[i];
-        __syncthreads();
-        // the boundary replay from the parent state (the queue holds only lanes the f32 loop accepted at the start)
-        int32_t* hrow = a.hidden + (size_t)chain * a.hist_stride + (size_t)p * a.N * C;
-        if (exact) {
-            const int an = checked_index(a.ancestry[(size_t)chain * a.anc_stride + (size_t)p * a.N + j], a.N);
-            const int32_t* hp = a.hidden + (size_t)chain * a.hist_stride + ((size_t)(p - 1) * a.N + an) * C;
-#pragma unroll
-            for (int c = 0; c < C; ++c) hrow[(size_t)j * C + c] = hp[c];
-        }
-        __syncthreads();
-        unsigned long long pend = __ballot(exact);
-        while (pend) {
-            const int L = (int)__builtin_ctzll(pend);
-            pend &= pend - 1ull;
-            const uint32_t jl = __builtin_amdgcn_readlane((uint32_t)j, L);
-            const int n = coop_replay<MODEL, G>(hrow + (size_t)jl * C, cp, jl, ptag, 1.0, tab);
-            if (tid == L) nev = n;
-        }
-        __syncthreads();
-        if (exact) {
-#pragma unroll
-            for (int c = 0; c < C; ++c) x[c] = (double)hrow[(size_t)j * C + c];
-        }
-    }
-    if (live) {
-        int32_t* hc = a.hidden + (size_t)chain * a.hist_stride + ((size_t)p * a.N + j) * C;
-#pragma unroll
-        for (int c = 0; c < C; ++c) hc[c] = (int32_t)x[c];
-    }
-    if (a.count_events) {   // the events after the first pass (a replayed lane's count is its whole step)
-        unsigned long long e = live ? (unsigned long long)(nev - rs.nev) : 0ull;
-        unsigned long long li = (unsigned long long)iters;
-        int wmax = iters;
-        for (int o = 32; o > 0; o >>= 1) {
-            e += __shfl_xor(e, o, 64);
-            li += __shfl_xor(li, o, 64);
-            wmax = max(wmax, __shfl_xor(wmax, o, 64));
-        }
-        if (tid == 0) {
-            unsigned long long* cs = counter_slot(a.counters);
-            atomicAdd(cs, e);
-            atomicAdd(cs + 2, li);
-            atomicAdd(cs + 3, 64ull * (unsigned long long)wmax);
-        }
-    }
-}
-
-// The compacting step's last pass: weights of the step's states against Y[p] and the in-block scan (what
-// pf_step_kernel does at its end otherwise), and the chain's queue reset for the next step.  Same grid as the step.
-template <int MODEL, int G, int OBS, int WG>
-__global__ __launch_bounds__(WG) void pf_weight_kernel(StepArgs a, int p) {
-    using Sh = Shape<MODEL, G>;
-    constexpr int C = Sh::C;
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    double* red = smem;
-    const BlockPos bp = step_block(a);
-    const int chain = bp.chain;
-    const int tid = threadIdx.x;
-    const int j = bp.b * WG + tid;
-    if (bp.b == 0 && tid == 0) a.qcount[chain] = 0;
-    if (a.status[chain] != 0 || p + 1 >= a.T) return;
-    const ChainParam cp = a.cp[chain];
-    const int cur = p & 1;
-    const size_t wcur = ((size_t)cur * a.max_chains + chain) * a.wstride;
-    const size_t bcur = ((size_t)cur * a.max_chains + chain) * a.bstride;
-    double w = 0.0;
-    if (j < a.N) {
-        const int32_t* hc = a.hidden + (size_t)chain * a.hist_stride + ((size_t)p * a.N + j) * C;
-        double x[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) x[c] = (double)hc[c];
-        w = particle_weight<MODEL, G, OBS>(x, a.Y + (size_t)p * Sh::K, cp, a.cp + chain, a.lf, a.lf_max, hc);
-    }
-    const double loc = block_inclusive_scan<WG>(w, red);
-    a.wraw[wcur + j] = w;
-    a.wloc[wcur + j] = loc;
-    if (tid == WG - 1) a.bsum[bcur + bp.b] = loc;
 }
 
 // particle_path_sampler, pmcmc.py:236-248 (one lane per chain; T dependent loads)
@@ -549,16 +394,8 @@ static hipError_t launch_filter_t(const StepArgs& a, int n_chains, const FilterS
             snprintf(msg, sizeof msg, "filter step %d group %d", p, g);
             EPIPF_RANGE_PUSH(msg);
 #endif
-            if (group) {
-                group(ag, p, grid, glds, s);
-            } else if (ag.compact > 0) {   // compacting step: first pass, continuation, weights
-                hipLaunchKernelGGL((pf_step_kernel<MODEL, G, OBS, WG, true>), grid, block, lds, s, ag, p);
-                hipLaunchKernelGGL((pf_resume_kernel<MODEL, G>), dim3(a.B * n_g), dim3(64), sizeof(LogTab) * kLogTabEntries,
-                                   s, ag, p, a.B);
-                hipLaunchKernelGGL((pf_weight_kernel<MODEL, G, OBS, WG>), grid, block, sizeof(double) * 16, s, ag, p);
-            } else {
-                hipLaunchKernelGGL((pf_step_kernel<MODEL, G, OBS, WG>), grid, block, lds, s, ag, p);
-            }
+            if (group) group(ag, p, grid, glds, s);
+            else hipLaunchKernelGGL((pf_step_kernel<MODEL, G, OBS, WG>), grid, block, lds, s, ag, p);
             EPIPF_RANGE_POP();
         }
         if (fs.g_end[g]) (void)hipEventRecord(fs.g_end[g], s);
